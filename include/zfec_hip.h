@@ -1,0 +1,135 @@
+/*
+ * zfec_hip.h -- C-ABI of libzfec_hip.so, the MI355X (gfx950) erasure-coding engine.
+ *
+ * Part 1 is a drop-in for zfec's own C interface (/root/reference/zfec/fec.h):
+ * same names, same argument meaning, same ownership rules, bit-identical
+ * results.  A program (or FFI binding: zfec/_fecmodule.c, haskell/Codec/FEC.hs)
+ * written against fec.h links against this library unchanged.  Buffers may be
+ * host memory or device memory (hipMalloc / torch CUDA tensors); the library
+ * detects which per pointer.  The GF(2^8) multiply-accumulate always runs in
+ * HIP kernels on the GPU -- there is no CPU compute path.
+ *
+ * Part 2 adds what a GPU caller needs: status codes instead of assert(),
+ * stream-ordered asynchronous variants, and batched strided entry points
+ * that encode/decode many independent stripes in one launch.
+ *
+ * Plain C types only (stream handles are passed as void*, i.e. hipStream_t).
+ */
+#ifndef ZFEC_HIP_H
+#define ZFEC_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* zfec/fec.h:9 */
+typedef unsigned char gf;
+
+/* zfec/fec.h:11-15.  The first three fields keep the reference layout (C callers
+ * may read k and n); `priv` is library-private and follows them. */
+typedef struct {
+    unsigned long magic;
+    unsigned short k, n; /* parameters of the code */
+    gf* enc_matrix;      /* n x k row-major systematic encoding matrix (host memory) */
+    void* priv;
+} fec_t;
+
+/* ---------------------------------------------------------------------------
+ * Part 1: zfec/fec.h drop-in
+ * ------------------------------------------------------------------------- */
+
+/* Replaces zfec/fec.h:33 / fec.c:406-413.  Builds the GF(2^8) tables.  Unlike
+ * the reference it is idempotent and thread-safe (std::call_once). */
+void fec_init(void);
+
+/* Replaces zfec/fec.h:39 / fec.c:430-479.  Returns NULL (and sets the
+ * thread-local status) on invalid parameters (k < 1, m > 256, k > m) instead
+ * of assert(); returns NULL if fec_init() was never called, like the reference
+ * (fec.c:442-444). */
+fec_t* fec_new(unsigned short k, unsigned short m);
+
+/* Replaces zfec/fec.h:40 / fec.c:423-428. */
+void fec_free(fec_t* p);
+
+/* Replaces zfec/fec.h:49 / fec.c:487-505.  fecs[i] receives block
+ * block_nums[i] (sz bytes) for i < num_block_nums.  Synchronous: the outputs
+ * are complete when it returns.  Errors (block number >= n, HIP failure) set
+ * the thread-local status and leave outputs unspecified; they never abort.
+ * Extension: a block number < k yields a copy of that primary block (the
+ * reference asserts, fec.c:498). */
+void fec_encode(const fec_t* code, const gf* const* src, gf* const* fecs,
+                const unsigned* block_nums, size_t num_block_nums, size_t sz);
+
+/* Replaces zfec/fec.h:57 / fec.c:527-557.  inpkts[i] holds block index[i];
+ * a present primary block i must sit at slot i.  outpkts receives the missing
+ * primaries in ascending order.  Synchronous. */
+void fec_decode(const fec_t* code, const gf* const* inpkts, gf* const* outpkts,
+                const unsigned* index, size_t sz);
+
+/* Exported by the reference too (fec.c:512-525, fec.c:341-394). */
+void build_decode_matrix_into_space(const fec_t* code, const unsigned* index, const unsigned k, gf* matrix);
+void _invert_vdm(gf* src, unsigned k);
+
+/* ---------------------------------------------------------------------------
+ * Part 2: extensions
+ * ------------------------------------------------------------------------- */
+
+enum {
+    FEC_OK = 0,
+    FEC_EINVAL = 1,     /* bad argument (k/m range, block number, duplicate, NULL) */
+    FEC_ENODEV = 2,     /* no usable GPU */
+    FEC_EHIP = 3,       /* a HIP runtime call failed */
+    FEC_ENOMEM = 4,     /* allocation failed */
+    FEC_ESINGULAR = 5,  /* decode matrix singular (duplicate block numbers) */
+    FEC_EUNINIT = 6     /* fec_init() not called */
+};
+
+#define FEC_FLAG_ASYNC 1u /* do not synchronize; all buffers must be device memory */
+
+/* Status of the last library call made by this thread, and its message. */
+int fec_last_status(void);
+const char* fec_last_error_message(void);
+
+/* fec_encode / fec_decode returning a status, on a caller-chosen HIP stream
+ * (NULL: the library's per-thread stream).  With FEC_FLAG_ASYNC and device
+ * buffers the call only enqueues work on `stream`. */
+int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fecs,
+                  const unsigned* block_nums, size_t num_block_nums, size_t sz,
+                  void* stream, unsigned flags);
+int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts,
+                  const unsigned* index, size_t sz, void* stream, unsigned flags);
+
+/* Batched encode of nstripes independent stripes in one launch (device memory
+ * only).  Block j of stripe s is read from src + s*src_stripe_stride +
+ * j*src_block_stride; output i of stripe s (block block_nums[i]) is written to
+ * dst + s*dst_stripe_stride + i*dst_block_stride.  Packed [stripe][block][sz]
+ * layouts use block_stride = sz, stripe_stride = k*sz (input) / num*sz (output). */
+int fec_encode_batch(const fec_t* code,
+                     const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                     gf* dst, size_t dst_block_stride, size_t dst_stripe_stride,
+                     const unsigned* block_nums, size_t num_block_nums, size_t sz,
+                     size_t nstripes, void* stream, unsigned flags);
+
+/* Batched decode: every stripe received the same block numbers (index[slot],
+ * primaries at their own slot as in fec_decode).  Slot j of stripe s at
+ * src + s*src_stripe_stride + j*src_block_stride; the recovered primaries
+ * (ascending) at dst + s*dst_stripe_stride + i*dst_block_stride. */
+int fec_decode_batch(const fec_t* code,
+                     const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                     gf* dst, size_t dst_block_stride, size_t dst_stripe_stride,
+                     const unsigned* index, size_t sz, size_t nstripes,
+                     void* stream, unsigned flags);
+
+/* Number of visible GPUs (0 when none; never aborts). */
+int fec_device_count(void);
+
+/* Library version string. */
+const char* fec_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZFEC_HIP_H */

@@ -1,0 +1,192 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports every
+symbol include/zfec_hip.h declares, the host-side matrix algebra matches the
+reference's golden vectors, and the Python surface validates arguments with
+the reference's error behaviour (zfec/test/test_zfec.py:85-105,162-258).
+No kernel launches here."""
+import ctypes
+import hashlib
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import zfec_amd
+from zfec_amd import capi
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "zfec_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src)))
+
+
+def test_header_symbols_exported():
+    names = header_functions()
+    assert "fec_encode" in names and "fec_decode" in names and "fec_encode_batch" in names
+    out = subprocess.run(["nm", "-D", "--defined-only", capi.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    L = capi.lib()
+    for n in names:
+        assert getattr(L, n) is not None
+    assert set(n for n, _, _ in capi.SYMBOLS) == set(names)
+
+
+def test_reference_fec_h_surface_subset():
+    # every function of zfec/fec.h (and the two non-static helpers of fec.c) is exported
+    for n in ["fec_init", "fec_new", "fec_free", "fec_encode", "fec_decode",
+              "build_decode_matrix_into_space", "_invert_vdm"]:
+        assert n in header_functions()
+
+
+def test_enc_matrix_matches_reference_every_k(golden):
+    meta, _ = golden
+    for k in range(1, 257):
+        E = capi.Code(k, 256).enc_matrix()
+        assert hashlib.sha256(E).hexdigest() == meta["enc_matrix_sha256_m256"][str(k)], k
+
+
+def test_enc_matrix_python_surface(golden):
+    _, arrays = golden
+    for key, E in arrays.items():
+        if key.startswith("enc_k"):
+            k, m = (int(x[1:]) for x in key[4:].split("_"))
+            got = np.frombuffer(zfec_amd.Encoder(k, m).enc_matrix(), dtype=np.uint8).reshape(m, k)
+            assert (got == E).all(), key
+
+
+def test_decode_matrix_rows(golden):
+    meta, arrays = golden
+    L = capi.lib()
+    for c in meta["decode_rows"]:
+        k, m, slots = c["k"], c["m"], c["slot_nums"]
+        code = capi.Code(k, m)
+        mat = (ctypes.c_ubyte * (k * k))()
+        L.build_decode_matrix_into_space(code.ptr, capi.uint_array(slots), k, ctypes.cast(mat, ctypes.c_void_p))
+        assert L.fec_last_status() == capi.FEC_OK
+        D = np.frombuffer(bytes(mat), dtype=np.uint8).reshape(k, k)
+        rows = D[[i for i in range(k) if slots[i] >= k]]
+        assert (rows == arrays[c["key"]]).all()
+
+
+def test_invert_vdm_matches_oracle():
+    L = capi.lib()
+    rng = np.random.default_rng(5)
+    for k in [1, 2, 3, 7, 20, 64]:
+        # a Vandermonde matrix of distinct points p_i (row i = p_i^j)
+        pts = rng.choice(np.arange(1, 256), size=k, replace=False).astype(np.uint8)
+        V = np.zeros((k, k), dtype=np.uint8)
+        for i in range(k):
+            acc = 1
+            for j in range(k):
+                V[i, j] = acc
+                acc = oracle.gf_mul(acc, int(pts[i]))
+        a = V.copy()
+        b = V.copy()
+        L._invert_vdm(a.ctypes.data_as(ctypes.c_void_p), k)
+        oracle.lib().oracle_invert_vdm(b.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), k)
+        assert (a == b).all(), k
+
+
+def test_fec_new_validation_no_abort():
+    L = capi.lib()
+    assert not L.fec_new(0, 3)
+    assert L.fec_last_status() == capi.FEC_EINVAL
+    assert not L.fec_new(4, 3)
+    assert not L.fec_new(1, 257)
+    p = L.fec_new(3, 10)
+    assert p
+    L.fec_free(p)
+
+
+def test_fec_encode_rejects_bad_block_number():
+    L = capi.lib()
+    code = capi.Code(3, 10)
+    src = [ctypes.create_string_buffer(8) for _ in range(3)]
+    dst = [ctypes.create_string_buffer(8)]
+    st = L.fec_encode_ex(code.ptr, capi.ptr_array([ctypes.addressof(b) for b in src]),
+                         capi.ptr_array([ctypes.addressof(b) for b in dst]), capi.uint_array([10]), 1, 8, None, 0)
+    assert st == capi.FEC_EINVAL
+
+
+def test_fec_decode_rejects_duplicates_and_misplaced_primaries():
+    L = capi.lib()
+    code = capi.Code(3, 10)
+    bufs = [ctypes.create_string_buffer(8) for _ in range(3)]
+    addrs = capi.ptr_array([ctypes.addressof(b) for b in bufs])
+    for idx in ([3, 3, 4], [1, 0, 5], [3, 4, 10]):
+        st = L.fec_decode_ex(code.ptr, addrs, addrs, capi.uint_array(idx), 8, None, 0)
+        assert st == capi.FEC_EINVAL, idx
+
+
+# ---- reference test_zfec.py argument tests, on our surface ------------------
+
+def test_instantiate_no_args():
+    with pytest.raises(TypeError):
+        zfec_amd.Encoder()
+    with pytest.raises(TypeError):
+        zfec_amd.Decoder()
+
+
+@pytest.mark.parametrize("cls", [zfec_amd.Encoder, zfec_amd.Decoder])
+def test_bad_args_construct(cls):
+    with pytest.raises(zfec_amd.Error, match="argument is required to be greater than or equal to 1"):
+        cls(-1, -1)
+    with pytest.raises(zfec_amd.Error, match="argument is required to be less than or equal to 256"):
+        cls(1, 257)
+    with pytest.raises(zfec_amd.Error, match="first argument is required to be less than or equal to the second argument"):
+        cls(3, 2)
+
+
+def test_bad_args_dec():
+    decer = zfec_amd.Decoder(2, 4)
+    with pytest.raises(TypeError, match="First argument was not a sequence"):
+        decer.decode(98, [])
+    with pytest.raises(zfec_amd.Error, match="Precondition violation: second argument is required to contain int"):
+        decer.decode(["a", "b"], ["c", "d"])
+    with pytest.raises(TypeError, match="Second argument was not a sequence"):
+        decer.decode(["a", "b"], 98)
+
+
+def test_bad_args_easyfec_dec():
+    decer = zfec_amd.easyfec.Decoder(2, 4)
+    with pytest.raises(TypeError, match="First argument was not a sequence"):
+        decer.decode(98, [0, 1], 0)
+    with pytest.raises(zfec_amd.Error, match="Precondition violation: second argument is required to contain int"):
+        decer.decode("ab", ["c", "d"], 0)
+    with pytest.raises(TypeError, match="Second argument was not a sequence"):
+        decer.decode("ab", 98, 0)
+
+
+def test_decode_rejects_what_reference_mishandles():
+    d = zfec_amd.Decoder(3, 5)
+    b = [b"x" * 4] * 3
+    with pytest.raises(zfec_amd.Error, match="greater than 255"):
+        d.decode(b, [0, 1, 256])
+    with pytest.raises(zfec_amd.Error, match="less than m"):
+        d.decode(b, [0, 1, 7])          # reference reads enc_matrix out of bounds
+    with pytest.raises(zfec_amd.Error, match="distinct"):
+        d.decode(b, [1, 1, 2])          # reference spins forever (_fecmodule.c:482-493)
+    e = zfec_amd.Encoder(3, 5)
+    with pytest.raises(zfec_amd.Error):
+        e.encode(b, [5])                # reference reads out of bounds
+    with pytest.raises(zfec_amd.Error, match="exactly k blocks"):
+        e.encode(b[:2])
+    with pytest.raises(zfec_amd.Error, match="same length"):
+        e.encode([b"a", b"bb", b"c"])
+
+
+@pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(zfec_amd.Error, match="no GPU"):
+        zfec_amd.Encoder(3, 10).encode([b"abc", b"def", b"ghi"])
+    with pytest.raises(zfec_amd.Error, match="no GPU"):
+        zfec_amd.Decoder(3, 10).decode([b"abc", b"def", b"ghi"], [3, 4, 5])
+    with pytest.raises(zfec_amd.Error, match="no GPU"):
+        zfec_amd.test_from_agl()

@@ -1,0 +1,162 @@
+"""zfec_amd -- zfec's erasure-coding API on AMD MI355X (gfx950).
+
+Drop-in for the reference's Python surface (/root/reference/zfec/__init__.py:12,
+zfec/_fecmodule.c): ``Encoder(k, m).encode(inblocks, desired_blocks_nums=None)``,
+``Decoder(k, m).decode(blocks, blocknums)``, ``Error``, ``easyfec``.
+
+Bytes-like blocks (bytes, bytearray, memoryview, C-contiguous numpy arrays)
+are staged to the GPU and the results come back as ``bytes``, exactly as the
+reference returns them.  Device-resident blocks (torch tensors on a ROCm
+device) stay on the device: the work is enqueued on the tensor's current
+stream and the results are new device tensors.  All GF(2^8) arithmetic runs
+in the HIP kernels of libzfec_hip.so; there is no CPU fallback -- importing
+fails if the extension is not built, and encode/decode raise ``Error`` when no
+GPU is visible.
+"""
+from . import _fec
+from ._fec import Error, device_count, test_from_agl, version
+
+__version__ = "0.1.0"
+
+__all__ = ["Encoder", "Decoder", "Error", "easyfec", "test_from_agl", "device_count", "version"]
+
+
+def _is_device_tensor(x):
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+def _byte_view(t):
+    import torch
+
+    if not t.is_contiguous():
+        raise Error("Precondition violation: Input blocks are required to be C-contiguous.")
+    return t.reshape(-1) if t.dtype == torch.uint8 else t.reshape(-1).view(torch.uint8)
+
+
+def _stream_handle(device):
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _device_blocks(blocks, k):
+    bl = [_byte_view(b) for b in blocks]
+    if len(bl) != k:
+        raise Error(
+            "Precondition violation: Wrong length -- first argument (the sequence of input blocks) is required to "
+            "contain exactly k blocks.  len(first): %d, k: %d" % (len(bl), k)
+        )
+    sz = bl[0].numel() if bl else 0
+    dev = bl[0].device if bl else None
+    for b in bl:
+        if b.numel() != sz:
+            raise Error(
+                "Precondition violation: Input blocks are required to be all the same length.  length of one block "
+                "was: %d, length of another block was: %d" % (sz, b.numel())
+            )
+        if b.device != dev:
+            raise Error("Precondition violation: device blocks are required to be on one device")
+    return bl, sz, dev
+
+
+class Encoder(_fec.Encoder):
+    """Encoder(k, m) -- see zfec/_fecmodule.c:40-44."""
+
+    def encode(self, inblocks, desired_blocks_nums=None):
+        try:
+            first = inblocks[0]
+        except Exception:
+            first = None
+        if first is None or not _is_device_tensor(first):
+            return _fec.Encoder.encode(self, inblocks, desired_blocks_nums)
+        return self._encode_device(list(inblocks), desired_blocks_nums)
+
+    def _encode_device(self, inblocks, desired):
+        import torch
+
+        k, m = self.k, self.m
+        if desired is None:
+            nums = list(range(m))
+        else:
+            try:
+                nums = list(desired)
+            except TypeError:
+                raise TypeError("Second argument (optional) was not a sequence.")
+            for x in nums:
+                if not isinstance(x, int):
+                    raise Error("Precondition violation: second argument is required to contain int.")
+                if x < 0 or x >= m:
+                    raise Error(
+                        "Precondition violation: desired block nums are required to be in [0, m-1] = [0, %d], "
+                        "but one was %d" % (m - 1, x)
+                    )
+        bl, sz, dev = _device_blocks(inblocks, k)
+        sec = [x for x in nums if x >= k]
+        outs = [torch.empty(sz, dtype=torch.uint8, device=dev) for _ in sec]
+        if sec and sz:
+            self.encode_into(
+                [b.data_ptr() for b in bl], [o.data_ptr() for o in outs], sec, sz, stream=_stream_handle(dev)
+            )
+        it = iter(outs)
+        return [inblocks[x] if x < k else next(it) for x in nums]
+
+
+class Decoder(_fec.Decoder):
+    """Decoder(k, m) -- see zfec/_fecmodule.c:321-325."""
+
+    def decode(self, blocks, blocknums):
+        try:
+            first = blocks[0]
+        except Exception:
+            first = None
+        if first is None or not _is_device_tensor(first):
+            return _fec.Decoder.decode(self, blocks, blocknums)
+        return self._decode_device(list(blocks), blocknums)
+
+    def _decode_device(self, blocks, blocknums):
+        import torch
+
+        k, m = self.k, self.m
+        try:
+            nums = list(blocknums)
+        except TypeError:
+            raise TypeError("Second argument was not a sequence.")
+        if len(nums) != k:
+            raise Error(
+                "Precondition violation: Wrong length -- blocknums is required to contain exactly k blocks.  "
+                "len(blocknums): %d, k: %d" % (len(nums), k)
+            )
+        for x in nums:
+            if not isinstance(x, int):
+                raise Error("Precondition violation: second argument is required to contain int.")
+            if x < 0 or x > 255:
+                raise Error("Precondition violation: block nums can't be less than zero or greater than 255.  %d\n" % x)
+            if x >= m:
+                raise Error(
+                    "Precondition violation: block nums are required to be less than m = %d, but one was %d" % (m, x)
+                )
+        if len(set(nums)) != k:
+            raise Error("Precondition violation: block nums are required to be distinct")
+        bl, sz, dev = _device_blocks(blocks, k)
+        objs = list(blocks)
+        # primary i into slot i (zfec/_fecmodule.c:482-493)
+        i = 0
+        while i < k:
+            c = nums[i]
+            if c >= k or c == i:
+                i += 1
+            else:
+                nums[i], nums[c] = nums[c], nums[i]
+                bl[i], bl[c] = bl[c], bl[i]
+                objs[i], objs[c] = objs[c], objs[i]
+        missing = [i for i in range(k) if nums[i] >= k]
+        outs = [torch.empty(sz, dtype=torch.uint8, device=dev) for _ in missing]
+        if missing and sz:
+            self.decode_into(
+                [b.data_ptr() for b in bl], [o.data_ptr() for o in outs], nums, sz, stream=_stream_handle(dev)
+            )
+        it = iter(outs)
+        return [objs[i] if nums[i] == i else next(it) for i in range(k)]
+
+
+from . import easyfec  # noqa: E402  (needs Encoder/Decoder above)

@@ -1,0 +1,115 @@
+"""ctypes binding of the C-ABI (include/zfec_hip.h) of libzfec_hip.so.
+
+This is the binding a ctypes/FFI user of zfec's fec.h would write (see
+INTEGRATION.md); tests use it to exercise the C entry points directly and
+bench.py uses the batched, stream-ordered extensions with device buffers.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzfec_hip.so")
+
+FEC_OK, FEC_EINVAL, FEC_ENODEV, FEC_EHIP, FEC_ENOMEM, FEC_ESINGULAR, FEC_EUNINIT = range(7)
+FEC_FLAG_ASYNC = 1
+
+# (name, restype, argtypes) for every symbol declared in include/zfec_hip.h
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_U = ctypes.c_uint
+_UP = ctypes.POINTER(ctypes.c_uint)
+_PP = ctypes.POINTER(ctypes.c_void_p)
+SYMBOLS = [
+    ("fec_init", None, []),
+    ("fec_new", _P, [ctypes.c_ushort, ctypes.c_ushort]),
+    ("fec_free", None, [_P]),
+    ("fec_encode", None, [_P, _PP, _PP, _UP, _SZ, _SZ]),
+    ("fec_decode", None, [_P, _PP, _PP, _UP, _SZ]),
+    ("build_decode_matrix_into_space", None, [_P, _UP, _U, _P]),
+    ("_invert_vdm", None, [_P, _U]),
+    ("fec_last_status", ctypes.c_int, []),
+    ("fec_last_error_message", ctypes.c_char_p, []),
+    ("fec_encode_ex", ctypes.c_int, [_P, _PP, _PP, _UP, _SZ, _SZ, _P, _U]),
+    ("fec_decode_ex", ctypes.c_int, [_P, _PP, _PP, _UP, _SZ, _P, _U]),
+    ("fec_encode_batch", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _SZ, _P, _U]),
+    ("fec_decode_batch", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _P, _U]),
+    ("fec_device_count", ctypes.c_int, []),
+    ("fec_version", ctypes.c_char_p, []),
+]
+
+
+class FecT(ctypes.Structure):
+    """Layout of fec_t (zfec/fec.h:11-15 prefix + priv)."""
+
+    _fields_ = [("magic", ctypes.c_ulong), ("k", ctypes.c_ushort), ("n", ctypes.c_ushort),
+                ("enc_matrix", ctypes.POINTER(ctypes.c_ubyte)), ("priv", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libzfec_hip.so is not built (run `make` or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        L.fec_init()
+        _lib = L
+    return _lib
+
+
+class FecError(RuntimeError):
+    pass
+
+
+def check(status):
+    if status != FEC_OK:
+        raise FecError("zfec-hip status %d: %s" % (status, lib().fec_last_error_message().decode()))
+
+
+def ptr_array(addrs):
+    return (ctypes.c_void_p * max(1, len(addrs)))(*addrs)
+
+
+def uint_array(vals):
+    return (ctypes.c_uint * max(1, len(vals)))(*vals)
+
+
+class Code(object):
+    """RAII wrapper around fec_t* (fec_new / fec_free)."""
+
+    def __init__(self, k, m):
+        self.k, self.m = k, m
+        self.ptr = lib().fec_new(k, m)
+        if not self.ptr:
+            raise FecError("fec_new(%d, %d) failed: %s" % (k, m, lib().fec_last_error_message().decode()))
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.fec_free(self.ptr)
+            self.ptr = None
+
+    def enc_matrix(self):
+        s = ctypes.cast(self.ptr, ctypes.POINTER(FecT)).contents
+        return bytes(s.enc_matrix[: self.k * self.m])
+
+    def encode_batch(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
+        check(lib().fec_encode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(block_nums),
+                                     len(block_nums), sz, nstripes, stream or None, flags))
+
+    def decode_batch(self, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
+        check(lib().fec_decode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(index),
+                                     sz, nstripes, stream or None, flags))
+
+    def encode_ptrs(self, in_addrs, out_addrs, block_nums, sz, stream=0, flags=FEC_FLAG_ASYNC):
+        check(lib().fec_encode_ex(self.ptr, ptr_array(in_addrs), ptr_array(out_addrs), uint_array(block_nums),
+                                  len(block_nums), sz, stream or None, flags))
+
+    def decode_ptrs(self, in_addrs, out_addrs, index, sz, stream=0, flags=FEC_FLAG_ASYNC):
+        check(lib().fec_decode_ex(self.ptr, ptr_array(in_addrs), ptr_array(out_addrs), uint_array(index),
+                                  sz, stream or None, flags))

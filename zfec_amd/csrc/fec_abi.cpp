@@ -1,0 +1,517 @@
+// fec_abi.cpp -- the C-ABI of libzfec_hip.so (include/zfec_hip.h).
+//
+// Part 1 replaces /root/reference/zfec/fec.h:33-57 (fec_init, fec_new,
+// fec_free, fec_encode, fec_decode) and the two helpers fec.c also exports.
+// Host-side work here is O(k^3) matrix algebra and argument checking; every
+// output byte is produced by the HIP kernels in kernels.hip.  Host buffers are
+// staged through per-thread device buffers; device buffers are used in place.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zfec_hip.h"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+#define FEC_API extern "C" __attribute__((visibility("default")))
+
+namespace zfec_hip {
+namespace {
+
+constexpr unsigned long kFecMagic = 0xFECC0DECUL;  // zfec/fec.c:421
+
+thread_local int t_status = FEC_OK;
+thread_local char t_msg[256] = "";
+
+int set_status(int st, const char* fmt = nullptr, ...) {
+    t_status = st;
+    if (fmt) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(t_msg, sizeof t_msg, fmt, ap);
+        va_end(ap);
+    } else {
+        t_msg[0] = '\0';
+    }
+    return st;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return set_status(FEC_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+unsigned long magic_of(const fec_t* p) {
+    return ((kFecMagic ^ p->k) ^ p->n) ^ reinterpret_cast<unsigned long>(p->enc_matrix);
+}
+
+bool valid_code(const fec_t* c) { return c && c->enc_matrix && c->magic == magic_of(c); }
+
+// ---- per-thread, per-device staging -----------------------------------------
+
+struct DevCtx {
+    hipStream_t stream = nullptr;
+    void* dbuf = nullptr;
+    size_t dcap = 0;
+    void* hbuf = nullptr;  // pinned
+    size_t hcap = 0;
+};
+
+struct ThreadCtx {
+    std::unordered_map<int, DevCtx> dev;
+    ~ThreadCtx() {
+        for (auto& kv : dev) {
+            int cur = 0;
+            if (hipGetDevice(&cur) != hipSuccess) continue;
+            if (hipSetDevice(kv.first) != hipSuccess) continue;
+            DevCtx& d = kv.second;
+            if (d.stream) (void)hipStreamDestroy(d.stream);
+            if (d.dbuf) (void)hipFree(d.dbuf);
+            if (d.hbuf) (void)hipHostFree(d.hbuf);
+            (void)hipSetDevice(cur);
+        }
+    }
+};
+
+thread_local ThreadCtx t_ctx;
+
+int dev_ctx(int device, DevCtx** out) {
+    DevCtx& d = t_ctx.dev[device];
+    if (!d.stream) {
+        hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamCreateWithFlags");
+    }
+    *out = &d;
+    return FEC_OK;
+}
+
+int ensure_dbuf(DevCtx& d, size_t bytes) {
+    if (bytes <= d.dcap) return FEC_OK;
+    if (d.dbuf) {
+        (void)hipStreamSynchronize(d.stream);
+        (void)hipFree(d.dbuf);
+        d.dbuf = nullptr;
+        d.dcap = 0;
+    }
+    const size_t cap = std::max<size_t>(bytes, 1u << 20);
+    hipError_t e = hipMalloc(&d.dbuf, cap);
+    if (e != hipSuccess) return set_status(FEC_ENOMEM, "hipMalloc(%zu): %s", cap, hipGetErrorString(e));
+    d.dcap = cap;
+    return FEC_OK;
+}
+
+int ensure_hbuf(DevCtx& d, size_t bytes) {
+    if (bytes <= d.hcap) return FEC_OK;
+    if (d.hbuf) {
+        (void)hipStreamSynchronize(d.stream);
+        (void)hipHostFree(d.hbuf);
+        d.hbuf = nullptr;
+        d.hcap = 0;
+    }
+    const size_t cap = std::max<size_t>(bytes, 1u << 20);
+    hipError_t e = hipHostMalloc(&d.hbuf, cap, hipHostMallocDefault);
+    if (e != hipSuccess) return set_status(FEC_ENOMEM, "hipHostMalloc(%zu): %s", cap, hipGetErrorString(e));
+    d.hcap = cap;
+    return FEC_OK;
+}
+
+// Device id of a device-accessible allocation, or -1 for host memory.
+int pointer_device(const void* p) {
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return a.device;
+    return -1;
+}
+
+int gpu_available() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+// RAII: restore the caller's current device.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// ---- the engine: apply an r x k matrix to k blocks -----------------------------
+//
+// in[j] / out[i] are device pointers (block bases of stripe 0); stripes are
+// in_sstride / out_sstride apart.  Splits into launches that respect the
+// kernel's limits: <= kMaxIn inputs (later input groups XOR-accumulate),
+// <= kMaxOut outputs and <= kMaxCoef coefficients per launch, and < 2^32
+// 16-byte units per launch.
+int apply_matrix(const uint8_t* coef /* r x k */, unsigned k, unsigned r, const uint8_t* const* in,
+                 uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
+                 hipStream_t stream) {
+    if (r == 0 || sz == 0 || nstripes == 0) return FEC_OK;
+    const size_t cps = (sz + kChunk - 1) / kChunk;
+    const size_t max_units = size_t(1) << 31;
+    const size_t stripes_per_launch = std::max<size_t>(1, max_units / cps);
+    if (cps > max_units) return set_status(FEC_EINVAL, "block size %zu too large for one launch", sz);
+    for (unsigned j0 = 0; j0 < k; j0 += kMaxIn) {
+        const unsigned kg = std::min<unsigned>(kMaxIn, k - j0);
+        const unsigned rmax = std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
+        for (unsigned i0 = 0; i0 < r; i0 += rmax) {
+            const unsigned rg = std::min<unsigned>(rmax, r - i0);
+            for (size_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
+                const size_t ns = std::min(stripes_per_launch, nstripes - s0);
+                MatJob job;
+                std::memset(&job, 0, sizeof job);
+                job.sz = sz;
+                job.in_sstride = in_sstride;
+                job.out_sstride = out_sstride;
+                job.nstripes = static_cast<uint32_t>(ns);
+                job.k = kg;
+                job.r = rg;
+                job.accumulate = j0 > 0;
+                for (unsigned j = 0; j < kg; ++j) job.in[j] = in[j0 + j] + s0 * in_sstride;
+                for (unsigned i = 0; i < rg; ++i) job.out[i] = out[i0 + i] + s0 * out_sstride;
+                for (unsigned i = 0; i < rg; ++i)
+                    for (unsigned j = 0; j < kg; ++j) job.coef[i * kg + j] = coef[size_t(i0 + i) * k + j0 + j];
+                hipError_t e = launch_matapply(job, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch_matapply");
+            }
+        }
+    }
+    return FEC_OK;
+}
+
+// ---- host/device pointer marshalling for the fec.h-shaped entry points -------
+
+struct Marshal {
+    int device = -1;
+    std::vector<const uint8_t*> din;
+    std::vector<uint8_t*> dout;
+    std::vector<int> in_host, out_host;  // indices of host-memory blocks
+};
+
+// Classify pointers and pick the device.  All device pointers must live on one device.
+int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marshal& m) {
+    m.in_host.clear();
+    m.out_host.clear();
+    int dev = -1;
+    auto visit = [&](const void* p, bool is_in, size_t idx) -> int {
+        if (!p) return set_status(FEC_EINVAL, "%s block %zu is NULL", is_in ? "input" : "output", idx);
+        const int d = pointer_device(p);
+        if (d < 0) {
+            (is_in ? m.in_host : m.out_host).push_back(static_cast<int>(idx));
+        } else if (dev < 0) {
+            dev = d;
+        } else if (d != dev) {
+            return set_status(FEC_EINVAL, "blocks live on different devices (%d, %d)", dev, d);
+        }
+        return FEC_OK;
+    };
+    for (size_t i = 0; i < nin; ++i)
+        if (visit(in[i], true, i)) return t_status;
+    for (size_t i = 0; i < nout; ++i)
+        if (visit(out[i], false, i)) return t_status;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return set_status(FEC_ENODEV, "no current HIP device");
+    m.device = dev;
+    return FEC_OK;
+}
+
+// Host blocks of up to this many bytes in total go through one pinned bounce
+// buffer (one H2D / D2H each way); larger ones are copied block by block.
+constexpr size_t kPackLimit = size_t(8) << 20;
+
+constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Run `coef` (r x k) over in -> out, staging host blocks.  Synchronous unless
+// FEC_FLAG_ASYNC and every block is device memory.
+int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out, size_t sz,
+               void* stream_arg, unsigned flags) {
+    if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
+    Marshal m;
+    if (classify(in, k, out, r, m)) return t_status;
+    DeviceGuard guard(m.device);
+    DevCtx* d = nullptr;
+    if (dev_ctx(m.device, &d)) return t_status;
+    hipStream_t st = stream_arg ? static_cast<hipStream_t>(stream_arg) : d->stream;
+    const bool any_host = !m.in_host.empty() || !m.out_host.empty();
+    if (sz == 0 || r == 0) return set_status(FEC_OK);
+
+    m.din.assign(in, in + k);
+    m.dout.assign(out, out + r);
+    const size_t slot = align_up(sz, 256);
+    const size_t nhost = m.in_host.size() + m.out_host.size();
+    hipError_t e;
+    if (nhost) {
+        if (ensure_dbuf(*d, slot * nhost)) return t_status;
+        uint8_t* base = static_cast<uint8_t*>(d->dbuf);
+        size_t si = 0;
+        for (int i : m.in_host) m.din[i] = base + slot * si++;
+        for (int i : m.out_host) m.dout[i] = base + slot * si++;
+        const bool pack = sz * nhost <= kPackLimit;
+        if (!m.in_host.empty()) {
+            if (pack) {
+                if (ensure_hbuf(*d, slot * m.in_host.size())) return t_status;
+                // the previous call on this thread has synchronised, so hbuf is free
+                uint8_t* hb = static_cast<uint8_t*>(d->hbuf);
+                for (size_t q = 0; q < m.in_host.size(); ++q) std::memcpy(hb + slot * q, in[m.in_host[q]], sz);
+                e = hipMemcpyAsync(base, hb, slot * m.in_host.size(), hipMemcpyHostToDevice, st);
+                if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
+            } else {
+                for (size_t q = 0; q < m.in_host.size(); ++q) {
+                    e = hipMemcpyAsync(base + slot * q, in[m.in_host[q]], sz, hipMemcpyHostToDevice, st);
+                    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
+                }
+            }
+        }
+    }
+    if (apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st)) return t_status;
+    if (!m.out_host.empty()) {
+        const size_t nin_h = m.in_host.size();
+        uint8_t* obase = static_cast<uint8_t*>(d->dbuf) + slot * nin_h;
+        const bool pack = sz * nhost <= kPackLimit;
+        if (pack) {
+            if (ensure_hbuf(*d, slot * std::max(m.out_host.size(), nin_h))) return t_status;
+            e = hipMemcpyAsync(d->hbuf, obase, slot * m.out_host.size(), hipMemcpyDeviceToHost, st);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
+            e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            const uint8_t* hb = static_cast<const uint8_t*>(d->hbuf);
+            for (size_t q = 0; q < m.out_host.size(); ++q) std::memcpy(out[m.out_host[q]], hb + slot * q, sz);
+        } else {
+            for (size_t q = 0; q < m.out_host.size(); ++q) {
+                e = hipMemcpyAsync(out[m.out_host[q]], obase + slot * q, sz, hipMemcpyDeviceToHost, st);
+                if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
+            }
+        }
+    }
+    if (any_host || !(flags & FEC_FLAG_ASYNC)) {
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    }
+    return set_status(FEC_OK);
+}
+
+int check_block_nums(const fec_t* code, const unsigned* nums, size_t num) {
+    if (num && !nums) return set_status(FEC_EINVAL, "block_nums is NULL");
+    for (size_t i = 0; i < num; ++i)
+        if (nums[i] >= code->n)
+            return set_status(FEC_EINVAL, "block number %u out of range (n = %u)", nums[i], unsigned(code->n));
+    return FEC_OK;
+}
+
+// Rows of the decode matrix for the missing primaries (ascending), r x k.
+int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& rows, unsigned& r) {
+    const unsigned k = code->k;
+    if (!index) return set_status(FEC_EINVAL, "index is NULL");
+    std::vector<unsigned char> seen(256, 0);
+    for (unsigned i = 0; i < k; ++i) {
+        if (index[i] >= code->n)
+            return set_status(FEC_EINVAL, "block number %u out of range (n = %u)", index[i], unsigned(code->n));
+        if (seen[index[i]]) return set_status(FEC_EINVAL, "duplicate block number %u", index[i]);
+        seen[index[i]] = 1;
+        if (index[i] < k && index[i] != i)
+            return set_status(FEC_EINVAL, "primary block %u must be at slot %u, found at slot %u", index[i], index[i], i);
+    }
+    std::vector<uint8_t> dec(size_t(k) * k);
+    if (!build_decode_matrix(code->enc_matrix, k, index, dec.data()))
+        return set_status(FEC_ESINGULAR, "decode matrix is singular");
+    rows.clear();
+    r = 0;
+    for (unsigned i = 0; i < k; ++i) {
+        if (index[i] < k) continue;
+        rows.insert(rows.end(), dec.begin() + size_t(i) * k, dec.begin() + size_t(i + 1) * k);
+        ++r;
+    }
+    return FEC_OK;
+}
+
+int encode_rows(const fec_t* code, const unsigned* nums, size_t num, std::vector<uint8_t>& rows) {
+    const unsigned k = code->k;
+    rows.resize(num * k);
+    for (size_t i = 0; i < num; ++i) std::memcpy(&rows[i * k], code->enc_matrix + size_t(nums[i]) * k, k);
+    return FEC_OK;
+}
+
+}  // namespace
+}  // namespace zfec_hip
+
+using namespace zfec_hip;
+
+// ============================================================================
+// Part 1: zfec/fec.h drop-in
+// ============================================================================
+
+FEC_API void fec_init(void) {
+    field_init();
+    set_status(FEC_OK);
+}
+
+FEC_API fec_t* fec_new(unsigned short k, unsigned short m) {
+    if (!field_ready()) {  // zfec/fec.c:442-444
+        set_status(FEC_EUNINIT, "fec_init() has not been called");
+        return nullptr;
+    }
+    if (k < 1 || m < 1 || m > 256 || k > m) {  // zfec/fec.c:437-440 (asserts there)
+        set_status(FEC_EINVAL, "invalid code parameters k=%u m=%u", unsigned(k), unsigned(m));
+        return nullptr;
+    }
+    fec_t* p = static_cast<fec_t*>(std::calloc(1, sizeof(fec_t)));
+    gf* enc = static_cast<gf*>(std::malloc(size_t(k) * m));
+    if (!p || !enc) {
+        std::free(p);
+        std::free(enc);
+        set_status(FEC_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    build_encoding_matrix(k, m, enc);
+    p->k = k;
+    p->n = m;
+    p->enc_matrix = enc;
+    p->priv = nullptr;
+    p->magic = magic_of(p);
+    set_status(FEC_OK);
+    return p;
+}
+
+FEC_API void fec_free(fec_t* p) {
+    if (!p) return;
+    if (!valid_code(p)) {  // zfec/fec.c:425 asserts; we refuse and report
+        set_status(FEC_EINVAL, "fec_free: bad magic");
+        return;
+    }
+    p->magic = 0;
+    std::free(p->enc_matrix);
+    std::free(p);
+    set_status(FEC_OK);
+}
+
+FEC_API int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fecs, const unsigned* block_nums,
+                          size_t num_block_nums, size_t sz, void* stream, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
+    if (num_block_nums == 0) return set_status(FEC_OK);
+    if (!src || !fecs) return set_status(FEC_EINVAL, "NULL block array");
+    std::vector<uint8_t> rows;
+    encode_rows(code, block_nums, num_block_nums, rows);
+    return run_single(rows.data(), code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
+}
+
+FEC_API void fec_encode(const fec_t* code, const gf* const* src, gf* const* fecs, const unsigned* block_nums,
+                        size_t num_block_nums, size_t sz) {
+    (void)fec_encode_ex(code, src, fecs, block_nums, num_block_nums, sz, nullptr, 0);
+}
+
+FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
+                          size_t sz, void* stream, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    std::vector<uint8_t> rows;
+    unsigned r = 0;
+    if (decode_rows(code, index, rows, r)) return t_status;
+    if (r == 0) return set_status(FEC_OK);
+    if (!inpkts || !outpkts) return set_status(FEC_EINVAL, "NULL block array");
+    return run_single(rows.data(), code->k, r, inpkts, outpkts, sz, stream, flags);
+}
+
+FEC_API void fec_decode(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
+                        size_t sz) {
+    (void)fec_decode_ex(code, inpkts, outpkts, index, sz, nullptr, 0);
+}
+
+FEC_API void build_decode_matrix_into_space(const fec_t* code, const unsigned* index, const unsigned k, gf* matrix) {
+    if (!valid_code(code) || k != code->k || !index || !matrix) {
+        set_status(FEC_EINVAL, "build_decode_matrix_into_space: bad arguments");
+        return;
+    }
+    for (unsigned i = 0; i < k; ++i)
+        if (index[i] >= code->n) {
+            set_status(FEC_EINVAL, "block number %u out of range", index[i]);
+            return;
+        }
+    if (!build_decode_matrix(code->enc_matrix, k, index, matrix))
+        set_status(FEC_ESINGULAR, "decode matrix is singular");
+    else
+        set_status(FEC_OK);
+}
+
+FEC_API void _invert_vdm(gf* src, unsigned k) {
+    field_init();
+    invert_vandermonde(src, k);
+}
+
+// ============================================================================
+// Part 2: extensions
+// ============================================================================
+
+FEC_API int fec_last_status(void) { return t_status; }
+FEC_API const char* fec_last_error_message(void) { return t_msg; }
+
+FEC_API int fec_device_count(void) { return gpu_available(); }
+
+FEC_API const char* fec_version(void) { return "zfec-hip 0.1.0 (gfx950)"; }
+
+namespace {
+int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src, size_t sbs, size_t sss, gf* dst,
+              size_t dbs, size_t dss, size_t sz, size_t nstripes, void* stream, unsigned flags) {
+    const unsigned k = code->k;
+    if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
+    if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    const int dev = pointer_device(src);
+    if (dev < 0 || pointer_device(dst) != dev)
+        return set_status(FEC_EINVAL, "batched entry points take device memory on one device");
+    DeviceGuard guard(dev);
+    DevCtx* d = nullptr;
+    if (dev_ctx(dev, &d)) return t_status;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+    std::vector<const uint8_t*> in(k);
+    std::vector<uint8_t*> out(r);
+    for (unsigned j = 0; j < k; ++j) in[j] = src + j * sbs;
+    for (unsigned i = 0; i < r; ++i) out[i] = dst + i * dbs;
+    if (apply_matrix(coef, k, r, in.data(), out.data(), sz, nstripes, sss, dss, st)) return t_status;
+    if (!(flags & FEC_FLAG_ASYNC)) {
+        hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    }
+    return set_status(FEC_OK);
+}
+}  // namespace
+
+FEC_API int fec_encode_batch(const fec_t* code, const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                             gf* dst, size_t dst_block_stride, size_t dst_stripe_stride, const unsigned* block_nums,
+                             size_t num_block_nums, size_t sz, size_t nstripes, void* stream, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
+    if (num_block_nums == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
+    std::vector<uint8_t> rows;
+    encode_rows(code, block_nums, num_block_nums, rows);
+    return run_batch(code, rows.data(), static_cast<unsigned>(num_block_nums), src, src_block_stride,
+                     src_stripe_stride, dst, dst_block_stride, dst_stripe_stride, sz, nstripes, stream, flags);
+}
+
+FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                             gf* dst, size_t dst_block_stride, size_t dst_stripe_stride, const unsigned* index,
+                             size_t sz, size_t nstripes, void* stream, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    std::vector<uint8_t> rows;
+    unsigned r = 0;
+    if (decode_rows(code, index, rows, r)) return t_status;
+    if (r == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
+    return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
+                     dst_stripe_stride, sz, nstripes, stream, flags);
+}

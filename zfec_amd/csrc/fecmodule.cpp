@@ -1,0 +1,599 @@
+// fecmodule.cpp -- zfec_amd._fec, the CPython surface of the engine.
+//
+// Mirrors /root/reference/zfec/_fecmodule.c: classes Encoder(k, m) and
+// Decoder(k, m) with .k/.m, Encoder.encode(inblocks, desired_blocks_nums=None),
+// Decoder.decode(blocks, blocknums), the exception Error and test_from_agl().
+// Argument checking and error strings follow _fecmodule.c:82-97,148-198,
+// 429-474; the inputs the reference mishandles (desired numbers >= m, decode
+// numbers in [m, 255], duplicate numbers, non-contiguous buffers) raise Error
+// here instead of reading out of bounds, hanging or aborting.
+//
+// The encode/decode work goes through libzfec_hip.so (fec_encode_ex /
+// fec_decode_ex) with the GIL released, as the reference does around
+// fec_encode/fec_decode (_fecmodule.c:221-223, 506-508).  Device-resident
+// blocks (torch tensors) use encode_into/decode_into with raw device addresses;
+// zfec_amd/__init__.py routes them there.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <structmember.h>
+
+#include <cstring>
+#include <vector>
+
+#include "../../include/zfec_hip.h"
+
+static PyObject* py_fec_error;
+
+namespace {
+
+struct Coder {
+    PyObject_HEAD
+    unsigned short kk;
+    unsigned short mm;
+    fec_t* fec_matrix;
+};
+
+PyObject* Coder_new(PyTypeObject* type, PyObject*, PyObject*) {
+    Coder* self = reinterpret_cast<Coder*>(type->tp_alloc(type, 0));
+    if (self) {
+        self->kk = 0;
+        self->mm = 0;
+        self->fec_matrix = nullptr;
+    }
+    return reinterpret_cast<PyObject*>(self);
+}
+
+int coder_init(Coder* self, PyObject* args, PyObject* kwdict, const char* fmt) {
+    static const char* kwlist[] = {"k", "m", nullptr};
+    int ink, inm;
+    if (!PyArg_ParseTupleAndKeywords(args, kwdict, fmt, const_cast<char**>(kwlist), &ink, &inm)) return -1;
+    // zfec/_fecmodule.c:82-97
+    if (ink < 1) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: first argument is required to be greater than or equal to 1, but it was %d",
+                     ink);
+        return -1;
+    }
+    if (inm < 1) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: second argument is required to be greater than or equal to 1, but it was %d",
+                     inm);
+        return -1;
+    }
+    if (inm > 256) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: second argument is required to be less than or equal to 256, but it was %d",
+                     inm);
+        return -1;
+    }
+    if (ink > inm) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: first argument is required to be less than or equal to the second "
+                     "argument, but they were %d and %d respectively",
+                     ink, inm);
+        return -1;
+    }
+    if (self->fec_matrix) {
+        fec_free(self->fec_matrix);
+        self->fec_matrix = nullptr;
+    }
+    self->kk = static_cast<unsigned short>(ink);
+    self->mm = static_cast<unsigned short>(inm);
+    fec_t* f;
+    Py_BEGIN_ALLOW_THREADS f = fec_new(self->kk, self->mm);
+    Py_END_ALLOW_THREADS if (!f) {
+        PyErr_Format(py_fec_error, "fec_new failed: %s", fec_last_error_message());
+        return -1;
+    }
+    self->fec_matrix = f;
+    return 0;
+}
+
+int Encoder_init(Coder* self, PyObject* args, PyObject* kw) { return coder_init(self, args, kw, "ii:Encoder.__init__"); }
+int Decoder_init(Coder* self, PyObject* args, PyObject* kw) { return coder_init(self, args, kw, "ii:Decoder.__init__"); }
+
+void Coder_dealloc(Coder* self) {
+    if (self->fec_matrix) fec_free(self->fec_matrix);
+    Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+bool ready(Coder* self) {
+    if (!self->fec_matrix) {
+        PyErr_SetString(py_fec_error, "coder is not initialised");
+        return false;
+    }
+    return true;
+}
+
+// Holds acquired buffers and releases them on scope exit.
+struct Buffers {
+    std::vector<Py_buffer> v;
+    explicit Buffers(size_t n) : v(n) {
+        for (auto& b : v) b.obj = nullptr;
+    }
+    ~Buffers() {
+        for (auto& b : v)
+            if (b.obj) PyBuffer_Release(&b);
+    }
+};
+
+// Parse a sequence of ints into `out`; false with an exception set.
+bool parse_nums(PyObject* fast, std::vector<long>& out) {
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+    PyObject** items = PySequence_Fast_ITEMS(fast);
+    out.resize(static_cast<size_t>(n));
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!PyLong_Check(items[i])) {
+            PyErr_Format(py_fec_error, "Precondition violation: second argument is required to contain int.");
+            return false;
+        }
+        out[i] = PyLong_AsLong(items[i]);
+        if (out[i] == -1 && PyErr_Occurred()) return false;
+    }
+    return true;
+}
+
+int raise_status(int st) {
+    PyErr_Format(py_fec_error, "zfec-hip error %d: %s", st, fec_last_error_message());
+    return -1;
+}
+
+// ---- Encoder.encode -----------------------------------------------------------
+// zfec/_fecmodule.c:116-260
+PyObject* Encoder_encode(Coder* self, PyObject* args) {
+    PyObject* inblocks;
+    PyObject* desired = nullptr;
+    if (!PyArg_ParseTuple(args, "O|O:Encoder.encode", &inblocks, &desired)) return nullptr;
+    if (!ready(self)) return nullptr;
+    const unsigned k = self->kk, m = self->mm;
+
+    std::vector<long> nums;
+    if (desired && desired != Py_None) {
+        PyObject* fd = PySequence_Fast(desired, "Second argument (optional) was not a sequence.");
+        if (!fd) return nullptr;
+        const bool ok = parse_nums(fd, nums);
+        Py_DECREF(fd);
+        if (!ok) return nullptr;
+        for (long x : nums)
+            if (x < 0 || x >= static_cast<long>(m)) {
+                PyErr_Format(py_fec_error,
+                             "Precondition violation: desired block nums are required to be in [0, m-1] = [0, %u], "
+                             "but one was %ld",
+                             m - 1, x);
+                return nullptr;
+            }
+    } else {
+        nums.resize(m);
+        for (unsigned i = 0; i < m; ++i) nums[i] = i;
+    }
+
+    PyObject* fast = PySequence_Fast(inblocks, "First argument was not a sequence.");
+    if (!fast) return nullptr;
+    if (PySequence_Fast_GET_SIZE(fast) != static_cast<Py_ssize_t>(k)) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: Wrong length -- first argument (the sequence of input blocks) is required "
+                     "to contain exactly k blocks.  len(first): %zd, k: %d",
+                     PySequence_Fast_GET_SIZE(fast), int(k));
+        Py_DECREF(fast);
+        return nullptr;
+    }
+    PyObject** items = PySequence_Fast_ITEMS(fast);
+    Buffers bufs(k);
+    std::vector<const gf*> in(k);
+    Py_ssize_t sz = -1;
+    for (unsigned i = 0; i < k; ++i) {
+        if (PyObject_GetBuffer(items[i], &bufs.v[i], PyBUF_SIMPLE)) {
+            bufs.v[i].obj = nullptr;
+            Py_DECREF(fast);
+            return nullptr;
+        }
+        if (!PyBuffer_IsContiguous(&bufs.v[i], 'C')) {
+            PyErr_Format(py_fec_error, "Precondition violation: Input blocks are required to be C-contiguous.");
+            Py_DECREF(fast);
+            return nullptr;
+        }
+        if (sz >= 0 && sz != bufs.v[i].len) {
+            PyErr_Format(py_fec_error,
+                         "Precondition violation: Input blocks are required to be all the same length.  length of one "
+                         "block was: %zd, length of another block was: %zd",
+                         sz, bufs.v[i].len);
+            Py_DECREF(fast);
+            return nullptr;
+        }
+        sz = bufs.v[i].len;
+        in[i] = static_cast<const gf*>(bufs.v[i].buf);
+    }
+    if (sz < 0) sz = 0;
+
+    // one fresh bytes object per requested secondary block (_fecmodule.c:206-217)
+    std::vector<unsigned> ids;
+    std::vector<PyObject*> produced;
+    std::vector<gf*> outp;
+    for (long x : nums)
+        if (x >= static_cast<long>(k)) {
+            PyObject* b = PyBytes_FromStringAndSize(nullptr, sz);
+            if (!b) {
+                for (PyObject* o : produced) Py_DECREF(o);
+                Py_DECREF(fast);
+                return nullptr;
+            }
+            ids.push_back(static_cast<unsigned>(x));
+            produced.push_back(b);
+            outp.push_back(reinterpret_cast<gf*>(PyBytes_AS_STRING(b)));
+        }
+    int st = FEC_OK;
+    if (!ids.empty()) {
+        Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, in.data(), outp.data(), ids.data(), ids.size(),
+                                                  static_cast<size_t>(sz), nullptr, 0);
+        Py_END_ALLOW_THREADS
+    }
+    if (st != FEC_OK) {
+        for (PyObject* o : produced) Py_DECREF(o);
+        Py_DECREF(fast);
+        raise_status(st);
+        return nullptr;
+    }
+    PyObject* result = PyList_New(static_cast<Py_ssize_t>(nums.size()));
+    if (!result) {
+        for (PyObject* o : produced) Py_DECREF(o);
+        Py_DECREF(fast);
+        return nullptr;
+    }
+    size_t ci = 0;
+    for (size_t i = 0; i < nums.size(); ++i) {
+        if (nums[i] < static_cast<long>(k)) {  // primaries by reference (_fecmodule.c:231-235)
+            PyObject* o = items[nums[i]];
+            Py_INCREF(o);
+            PyList_SET_ITEM(result, static_cast<Py_ssize_t>(i), o);
+        } else {
+            PyList_SET_ITEM(result, static_cast<Py_ssize_t>(i), produced[ci++]);
+        }
+    }
+    Py_DECREF(fast);
+    return result;
+}
+
+// ---- Decoder.decode -----------------------------------------------------------
+// zfec/_fecmodule.c:400-544
+PyObject* Decoder_decode(Coder* self, PyObject* args) {
+    PyObject *blocks, *blocknums;
+    if (!PyArg_ParseTuple(args, "OO:Decoder.decode", &blocks, &blocknums)) return nullptr;
+    if (!ready(self)) return nullptr;
+    const unsigned k = self->kk, m = self->mm;
+
+    PyObject* fb = PySequence_Fast(blocks, "First argument was not a sequence.");
+    if (!fb) return nullptr;
+    PyObject* fn = PySequence_Fast(blocknums, "Second argument was not a sequence.");
+    if (!fn) {
+        Py_DECREF(fb);
+        return nullptr;
+    }
+    struct Drop {
+        PyObject *a, *b;
+        ~Drop() {
+            Py_XDECREF(a);
+            Py_XDECREF(b);
+        }
+    } drop{fb, fn};
+
+    if (PySequence_Fast_GET_SIZE(fb) != static_cast<Py_ssize_t>(k)) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: Wrong length -- first argument is required to contain exactly k blocks.  "
+                     "len(first): %zd, k: %d",
+                     PySequence_Fast_GET_SIZE(fb), int(k));
+        return nullptr;
+    }
+    if (PySequence_Fast_GET_SIZE(fn) != static_cast<Py_ssize_t>(k)) {
+        PyErr_Format(py_fec_error,
+                     "Precondition violation: Wrong length -- blocknums is required to contain exactly k blocks.  "
+                     "len(blocknums): %zd, k: %d",
+                     PySequence_Fast_GET_SIZE(fn), int(k));
+        return nullptr;
+    }
+    std::vector<long> nums;
+    if (!parse_nums(fn, nums)) return nullptr;
+    std::vector<unsigned char> seen(256, 0);
+    for (long x : nums) {
+        if (x < 0 || x > 255) {  // _fecmodule.c:459-462
+            PyErr_Format(py_fec_error,
+                         "Precondition violation: block nums can't be less than zero or greater than 255.  %ld\n", x);
+            return nullptr;
+        }
+        if (x >= static_cast<long>(m)) {
+            PyErr_Format(py_fec_error,
+                         "Precondition violation: block nums are required to be less than m = %u, but one was %ld", m, x);
+            return nullptr;
+        }
+        if (seen[x]) {
+            PyErr_Format(py_fec_error, "Precondition violation: block nums are required to be distinct, but %ld repeats",
+                         x);
+            return nullptr;
+        }
+        seen[x] = 1;
+    }
+    PyObject** items = PySequence_Fast_ITEMS(fb);
+    Buffers bufs(k);
+    std::vector<const gf*> cblocks(k);
+    std::vector<PyObject*> objs(items, items + k);
+    std::vector<unsigned> cnums(k);
+    Py_ssize_t sz = -1;
+    for (unsigned i = 0; i < k; ++i) {
+        if (PyObject_GetBuffer(items[i], &bufs.v[i], PyBUF_SIMPLE)) {
+            bufs.v[i].obj = nullptr;
+            return nullptr;
+        }
+        if (!PyBuffer_IsContiguous(&bufs.v[i], 'C')) {
+            PyErr_Format(py_fec_error, "Precondition violation: Input blocks are required to be C-contiguous.");
+            return nullptr;
+        }
+        if (sz >= 0 && sz != bufs.v[i].len) {
+            PyErr_Format(py_fec_error,
+                         "Precondition violation: Input blocks are required to be all the same length.  length of one "
+                         "block was: %zd, length of another block was: %zd\n",
+                         sz, bufs.v[i].len);
+            return nullptr;
+        }
+        sz = bufs.v[i].len;
+        cblocks[i] = static_cast<const gf*>(bufs.v[i].buf);
+        cnums[i] = static_cast<unsigned>(nums[i]);
+    }
+    if (sz < 0) sz = 0;
+    // move primary i to slot i (_fecmodule.c:482-493); numbers are distinct, so this terminates
+    for (unsigned i = 0; i < k;) {
+        if (cnums[i] >= k || cnums[i] == i) {
+            ++i;
+        } else {
+            const unsigned c = cnums[i];
+            std::swap(cnums[i], cnums[c]);
+            std::swap(cblocks[i], cblocks[c]);
+            std::swap(objs[i], objs[c]);
+        }
+    }
+    std::vector<PyObject*> rec;
+    std::vector<gf*> recp;
+    for (unsigned i = 0; i < k; ++i)
+        if (cnums[i] >= k) {
+            PyObject* b = PyBytes_FromStringAndSize(nullptr, sz);
+            if (!b) {
+                for (PyObject* o : rec) Py_DECREF(o);
+                return nullptr;
+            }
+            rec.push_back(b);
+            recp.push_back(reinterpret_cast<gf*>(PyBytes_AS_STRING(b)));
+        }
+    int st = FEC_OK;
+    if (!rec.empty()) {
+        Py_BEGIN_ALLOW_THREADS st =
+            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, 0);
+        Py_END_ALLOW_THREADS
+    }
+    if (st != FEC_OK) {
+        for (PyObject* o : rec) Py_DECREF(o);
+        raise_status(st);
+        return nullptr;
+    }
+    PyObject* result = PyList_New(k);
+    if (!result) {
+        for (PyObject* o : rec) Py_DECREF(o);
+        return nullptr;
+    }
+    size_t ri = 0;
+    for (unsigned i = 0; i < k; ++i) {
+        if (cnums[i] == i) {
+            Py_INCREF(objs[i]);
+            PyList_SET_ITEM(result, i, objs[i]);
+        } else {
+            PyList_SET_ITEM(result, i, rec[ri++]);
+        }
+    }
+    return result;
+}
+
+// ---- device-address entry points (used by zfec_amd for torch tensors) ---------
+
+bool addr_list(PyObject* seq, std::vector<void*>& out, const char* what) {
+    PyObject* f = PySequence_Fast(seq, what);
+    if (!f) return false;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(f);
+    out.resize(static_cast<size_t>(n));
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        out[i] = PyLong_AsVoidPtr(PySequence_Fast_GET_ITEM(f, i));
+        if (PyErr_Occurred()) {
+            Py_DECREF(f);
+            return false;
+        }
+    }
+    Py_DECREF(f);
+    return true;
+}
+
+bool uint_list(PyObject* seq, std::vector<unsigned>& out, const char* what) {
+    PyObject* f = PySequence_Fast(seq, what);
+    if (!f) return false;
+    std::vector<long> v;
+    const bool ok = parse_nums(f, v);
+    Py_DECREF(f);
+    if (!ok) return false;
+    out.assign(v.begin(), v.end());
+    for (long x : v)
+        if (x < 0 || x > 255) {
+            PyErr_Format(py_fec_error, "Precondition violation: block nums can't be less than zero or greater than 255.  %ld\n", x);
+            return false;
+        }
+    return true;
+}
+
+// encode_into(in_addrs, out_addrs, block_nums, sz, stream=0, sync=False)
+PyObject* Encoder_encode_into(Coder* self, PyObject* args, PyObject* kw) {
+    static const char* kwlist[] = {"in_addrs", "out_addrs", "block_nums", "sz", "stream", "sync", nullptr};
+    PyObject *pin, *pout, *pnums;
+    unsigned long long sz = 0, stream = 0;
+    int sync = 0;
+    if (!PyArg_ParseTupleAndKeywords(args, kw, "OOOK|Kp:Encoder.encode_into", const_cast<char**>(kwlist), &pin, &pout,
+                                     &pnums, &sz, &stream, &sync))
+        return nullptr;
+    if (!ready(self)) return nullptr;
+    std::vector<void*> in, out;
+    std::vector<unsigned> nums;
+    if (!addr_list(pin, in, "in_addrs must be a sequence") || !addr_list(pout, out, "out_addrs must be a sequence") ||
+        !uint_list(pnums, nums, "block_nums must be a sequence"))
+        return nullptr;
+    if (in.size() != self->kk || out.size() != nums.size()) {
+        PyErr_Format(py_fec_error, "Precondition violation: need k=%d inputs and one output per block num", int(self->kk));
+        return nullptr;
+    }
+    int st;
+    Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, reinterpret_cast<const gf* const*>(in.data()),
+                                              reinterpret_cast<gf* const*>(out.data()), nums.data(), nums.size(), sz,
+                                              reinterpret_cast<void*>(stream), sync ? 0u : FEC_FLAG_ASYNC);
+    Py_END_ALLOW_THREADS if (st != FEC_OK) {
+        raise_status(st);
+        return nullptr;
+    }
+    Py_RETURN_NONE;
+}
+
+// decode_into(in_addrs, out_addrs, slot_nums, sz, stream=0, sync=False): slots already ordered
+PyObject* Decoder_decode_into(Coder* self, PyObject* args, PyObject* kw) {
+    static const char* kwlist[] = {"in_addrs", "out_addrs", "slot_nums", "sz", "stream", "sync", nullptr};
+    PyObject *pin, *pout, *pnums;
+    unsigned long long sz = 0, stream = 0;
+    int sync = 0;
+    if (!PyArg_ParseTupleAndKeywords(args, kw, "OOOK|Kp:Decoder.decode_into", const_cast<char**>(kwlist), &pin, &pout,
+                                     &pnums, &sz, &stream, &sync))
+        return nullptr;
+    if (!ready(self)) return nullptr;
+    std::vector<void*> in, out;
+    std::vector<unsigned> nums;
+    if (!addr_list(pin, in, "in_addrs must be a sequence") || !addr_list(pout, out, "out_addrs must be a sequence") ||
+        !uint_list(pnums, nums, "slot_nums must be a sequence"))
+        return nullptr;
+    if (in.size() != self->kk || nums.size() != self->kk) {
+        PyErr_Format(py_fec_error, "Precondition violation: need k=%d inputs and slot nums", int(self->kk));
+        return nullptr;
+    }
+    int st;
+    Py_BEGIN_ALLOW_THREADS st = fec_decode_ex(self->fec_matrix, reinterpret_cast<const gf* const*>(in.data()),
+                                              reinterpret_cast<gf* const*>(out.data()), nums.data(), sz,
+                                              reinterpret_cast<void*>(stream), sync ? 0u : FEC_FLAG_ASYNC);
+    Py_END_ALLOW_THREADS if (st != FEC_OK) {
+        raise_status(st);
+        return nullptr;
+    }
+    Py_RETURN_NONE;
+}
+
+PyObject* Coder_enc_matrix(Coder* self, PyObject*) {
+    if (!ready(self)) return nullptr;
+    return PyBytes_FromStringAndSize(reinterpret_cast<const char*>(self->fec_matrix->enc_matrix),
+                                     Py_ssize_t(self->kk) * self->mm);
+}
+
+const char Encoder_doc[] =
+    "Encoder(k, m): systematic Reed-Solomon encoder over GF(2^8) running on MI355X.\n\n"
+    "@param k: the number of packets required for reconstruction\n"
+    "@param m: the number of packets generated\n";
+const char Decoder_doc[] =
+    "Decoder(k, m): recovers the k primary blocks from any k of the m blocks (MI355X).\n\n"
+    "@param k: the number of packets required for reconstruction\n"
+    "@param m: the number of packets generated\n";
+const char encode_doc[] =
+    "encode(inblocks, desired_blocks_nums=None) -> list of blocks.\n"
+    "Primary blocks in the result are the very objects passed in; secondary blocks are new bytes.";
+const char decode_doc[] =
+    "decode(blocks, blocknums) -> the k primary blocks in order.\n"
+    "Primary blocks present in the input are returned by reference; recovered ones are new bytes.";
+
+PyMethodDef Encoder_methods[] = {
+    {"encode", reinterpret_cast<PyCFunction>(Encoder_encode), METH_VARARGS, encode_doc},
+    {"encode_into", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(Encoder_encode_into)),
+     METH_VARARGS | METH_KEYWORDS, "Encode device-resident blocks given raw device addresses (stream-ordered)."},
+    {"enc_matrix", reinterpret_cast<PyCFunction>(Coder_enc_matrix), METH_NOARGS, "The m x k encoding matrix as bytes."},
+    {nullptr, nullptr, 0, nullptr}};
+PyMethodDef Decoder_methods[] = {
+    {"decode", reinterpret_cast<PyCFunction>(Decoder_decode), METH_VARARGS, decode_doc},
+    {"decode_into", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(Decoder_decode_into)),
+     METH_VARARGS | METH_KEYWORDS, "Decode device-resident blocks given raw device addresses (stream-ordered)."},
+    {"enc_matrix", reinterpret_cast<PyCFunction>(Coder_enc_matrix), METH_NOARGS, "The m x k encoding matrix as bytes."},
+    {nullptr, nullptr, 0, nullptr}};
+PyMemberDef Coder_members[] = {
+    {const_cast<char*>("k"), T_USHORT, offsetof(Coder, kk), READONLY, const_cast<char*>("k")},
+    {const_cast<char*>("m"), T_USHORT, offsetof(Coder, mm), READONLY, const_cast<char*>("m")},
+    {nullptr, 0, 0, 0, nullptr}};
+
+PyTypeObject Encoder_type = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject Decoder_type = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// zfec/_fecmodule.c:614-659: k=3, n=5, 8-byte blocks of 0x01/0x02/0x03; encode
+// blocks 3 and 4, decode primaries 0 and 1 from {3, 4, 2}, compare.
+PyObject* test_from_agl(PyObject*, PyObject*) {
+    unsigned char b0[8], b1[8], b2[8], b3[8], b4[8], b0c[8], b1c[8];
+    std::memset(b0, 1, 8);
+    std::memset(b1, 2, 8);
+    std::memset(b2, 3, 8);
+    const gf* blocks[3] = {b0, b1, b2};
+    gf* outblocks[2] = {b3, b4};
+    unsigned block_nums[2] = {3, 4};
+    fec_t* f = fec_new(3, 5);
+    if (!f) return PyErr_Format(py_fec_error, "fec_new: %s", fec_last_error_message());
+    int st = fec_encode_ex(f, blocks, outblocks, block_nums, 2, 8, nullptr, 0);
+    std::memcpy(b0c, b0, 8);
+    std::memcpy(b1c, b1, 8);
+    const gf* inpkts[3] = {b3, b4, b2};
+    gf* outpkts[2] = {b0, b1};
+    unsigned indexes[3] = {3, 4, 2};
+    if (st == FEC_OK) st = fec_decode_ex(f, inpkts, outpkts, indexes, 8, nullptr, 0);
+    if (st != FEC_OK) {
+        raise_status(st);  // before fec_free, which resets the thread's status
+        fec_free(f);
+        return nullptr;
+    }
+    fec_free(f);
+    if (std::memcmp(b0, b0c, 8) == 0 && std::memcmp(b1, b1c, 8) == 0) Py_RETURN_TRUE;
+    Py_RETURN_FALSE;
+}
+
+PyObject* py_device_count(PyObject*, PyObject*) { return PyLong_FromLong(fec_device_count()); }
+PyObject* py_version(PyObject*, PyObject*) { return PyUnicode_FromString(fec_version()); }
+
+PyMethodDef module_functions[] = {
+    {"test_from_agl", test_from_agl, METH_NOARGS, "Encode/decode round trip of zfec's C self-test (on the GPU)."},
+    {"device_count", py_device_count, METH_NOARGS, "Number of visible GPUs."},
+    {"version", py_version, METH_NOARGS, "Library version."},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef moduledef = {PyModuleDef_HEAD_INIT, "_fec", "FEC - Forward Error Correction on MI355X", -1,
+                         module_functions};
+
+void fill_type(PyTypeObject& t, const char* name, const char* doc, initproc init, PyMethodDef* methods) {
+    t.tp_name = name;
+    t.tp_basicsize = sizeof(Coder);
+    t.tp_dealloc = reinterpret_cast<destructor>(Coder_dealloc);
+    t.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE;
+    t.tp_doc = doc;
+    t.tp_methods = methods;
+    t.tp_members = Coder_members;
+    t.tp_init = init;
+    t.tp_new = Coder_new;
+}
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fec(void) {
+    fill_type(Encoder_type, "zfec_amd._fec.Encoder", Encoder_doc, reinterpret_cast<initproc>(Encoder_init),
+              Encoder_methods);
+    fill_type(Decoder_type, "zfec_amd._fec.Decoder", Decoder_doc, reinterpret_cast<initproc>(Decoder_init),
+              Decoder_methods);
+    if (PyType_Ready(&Encoder_type) < 0 || PyType_Ready(&Decoder_type) < 0) return nullptr;
+    PyObject* module = PyModule_Create(&moduledef);
+    if (!module) return nullptr;
+    Py_INCREF(&Encoder_type);
+    Py_INCREF(&Decoder_type);
+    PyModule_AddObject(module, "Encoder", reinterpret_cast<PyObject*>(&Encoder_type));
+    PyModule_AddObject(module, "Decoder", reinterpret_cast<PyObject*>(&Decoder_type));
+    py_fec_error = PyErr_NewException("zfec_amd.Error", nullptr, nullptr);
+    Py_INCREF(py_fec_error);
+    PyModule_AddObject(module, "Error", py_fec_error);
+    fec_init();
+    return module;
+}

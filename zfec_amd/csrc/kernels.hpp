@@ -1,0 +1,47 @@
+// kernels.hpp -- launch interface of the GF(2^8) matrix-apply kernels.
+//
+// One kernel family serves both directions of the code:
+//   encode: out_i = sum_j E[block_nums[i]][j] * in_j   (zfec/fec.c:487-505)
+//   decode: out_r = sum_c D[r][c] * in_c                (zfec/fec.c:527-557)
+// i.e. an r x k coefficient matrix applied byte-wise to k input blocks, for
+// `nstripes` independent stripes that share the matrix.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace zfec_hip {
+
+constexpr int kMaxIn = 32;     // input blocks per launch (larger k: XOR-accumulating passes)
+constexpr int kMaxOut = 48;    // output blocks per launch
+constexpr int kMaxCoef = 1536; // r*k coefficients per launch
+constexpr int kChunk = 16;     // bytes per lane per block per step (one dwordx4)
+constexpr int kBlock = 256;    // threads per workgroup
+
+// Kernel argument block (passed by value; ~2.2 KiB, well inside the kernarg limit).
+struct alignas(16) MatJob {
+    uint64_t sz;           // bytes per block
+    uint64_t in_sstride;   // stripe stride added to every input pointer
+    uint64_t out_sstride;  // stripe stride added to every output pointer
+    uint32_t nstripes;
+    uint32_t k;            // inputs in this launch
+    uint32_t r;            // outputs in this launch
+    uint32_t cps;          // 16-byte chunks per stripe = ceil(sz / 16)
+    uint32_t gs_c, gs_s;   // grid stride expressed as (chunks, stripes): stride = gs_s*cps + gs_c
+    uint32_t accumulate;   // 1: out ^= result (continuation pass for k > kMaxIn)
+    uint32_t pad_;
+    const uint8_t* in[kMaxIn];
+    uint8_t* out[kMaxOut];
+    uint8_t coef[kMaxCoef];  // r x k, row-major
+};
+
+// Enqueue one launch on `stream`.  Validates shapes against the kernel's
+// compile-time limits before launching (returns hipErrorInvalidValue
+// otherwise); chooses the specialised variant for (k, r) when one exists.
+hipError_t launch_matapply(MatJob& job, hipStream_t stream);
+
+// Name of the variant launch_matapply would use (for tests / profiling).
+const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
+
+}  // namespace zfec_hip
