@@ -14,7 +14,7 @@ EXT      := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('E
 SRC      := zfec_amd/csrc
 LIB      := zfec_amd/libzfec_hip.so
 PYEXT    := zfec_amd/_fec$(EXT)
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function
+HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function
 
 all: $(LIB) $(PYEXT) oracle
 

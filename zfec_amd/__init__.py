@@ -13,7 +13,11 @@ in the HIP kernels of libzfec_hip.so; there is no CPU fallback -- importing
 fails if the extension is not built, and encode/decode raise ``Error`` when no
 GPU is visible.
 """
-from . import _fec
+from . import _runtime
+
+_runtime.preload()  # must precede loading libzfec_hip.so (see _runtime.py)
+
+from . import _fec  # noqa: E402
 from ._fec import Error, device_count, test_from_agl, version
 
 __version__ = "0.1.0"

@@ -53,6 +53,9 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError("libzfec_hip.so is not built (run `make` or __graft_entry__.build())")
+        from . import _runtime
+
+        _runtime.preload()
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SYMBOLS:
             f = getattr(L, name)
