@@ -86,15 +86,19 @@ enum {
     FEC_EUNINIT = 6     /* fec_init() not called */
 };
 
-#define FEC_FLAG_ASYNC 1u /* do not synchronize; all buffers must be device memory */
+#define FEC_FLAG_ASYNC 1u          /* do not synchronize; all buffers must be device memory */
+#define FEC_FLAG_LIBRARY_STREAM 2u /* ignore `stream`; use the library's per-thread stream */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);
 const char* fec_last_error_message(void);
 
-/* fec_encode / fec_decode returning a status, on a caller-chosen HIP stream
- * (NULL: the library's per-thread stream).  With FEC_FLAG_ASYNC and device
- * buffers the call only enqueues work on `stream`. */
+/* fec_encode / fec_decode returning a status, on a caller-chosen HIP stream.
+ * `stream` follows HIP's convention: NULL is the null (legacy default) stream,
+ * which is what torch's default stream hands out.  FEC_FLAG_LIBRARY_STREAM
+ * selects the library's own per-thread non-blocking stream instead (what the
+ * synchronous fec_encode / fec_decode use).  With FEC_FLAG_ASYNC and device
+ * buffers the call only enqueues work on the stream. */
 int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fecs,
                   const unsigned* block_nums, size_t num_block_nums, size_t sz,
                   void* stream, unsigned flags);

@@ -249,7 +249,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     DeviceGuard guard(m.device);
     DevCtx* d = nullptr;
     if (dev_ctx(m.device, &d)) return t_status;
-    hipStream_t st = stream_arg ? static_cast<hipStream_t>(stream_arg) : d->stream;
+    hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream_arg);
     const bool any_host = !m.in_host.empty() || !m.out_host.empty();
     if (sz == 0 || r == 0) return set_status(FEC_OK);
 
@@ -415,7 +415,7 @@ FEC_API int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fe
 
 FEC_API void fec_encode(const fec_t* code, const gf* const* src, gf* const* fecs, const unsigned* block_nums,
                         size_t num_block_nums, size_t sz) {
-    (void)fec_encode_ex(code, src, fecs, block_nums, num_block_nums, sz, nullptr, 0);
+    (void)fec_encode_ex(code, src, fecs, block_nums, num_block_nums, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
 }
 
 FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
@@ -431,7 +431,7 @@ FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const*
 
 FEC_API void fec_decode(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
                         size_t sz) {
-    (void)fec_decode_ex(code, inpkts, outpkts, index, sz, nullptr, 0);
+    (void)fec_decode_ex(code, inpkts, outpkts, index, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
 }
 
 FEC_API void build_decode_matrix_into_space(const fec_t* code, const unsigned* index, const unsigned k, gf* matrix) {
@@ -478,7 +478,7 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     DeviceGuard guard(dev);
     DevCtx* d = nullptr;
     if (dev_ctx(dev, &d)) return t_status;
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : d->stream;
+    hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
     std::vector<const uint8_t*> in(k);
     std::vector<uint8_t*> out(r);
     for (unsigned j = 0; j < k; ++j) in[j] = src + j * sbs;

@@ -224,7 +224,7 @@ PyObject* Encoder_encode(Coder* self, PyObject* args) {
     int st = FEC_OK;
     if (!ids.empty()) {
         Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, in.data(), outp.data(), ids.data(), ids.size(),
-                                                  static_cast<size_t>(sz), nullptr, 0);
+                                                  static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
@@ -364,7 +364,7 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
     int st = FEC_OK;
     if (!rec.empty()) {
         Py_BEGIN_ALLOW_THREADS st =
-            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, 0);
+            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
@@ -536,13 +536,13 @@ PyObject* test_from_agl(PyObject*, PyObject*) {
     unsigned block_nums[2] = {3, 4};
     fec_t* f = fec_new(3, 5);
     if (!f) return PyErr_Format(py_fec_error, "fec_new: %s", fec_last_error_message());
-    int st = fec_encode_ex(f, blocks, outblocks, block_nums, 2, 8, nullptr, 0);
+    int st = fec_encode_ex(f, blocks, outblocks, block_nums, 2, 8, nullptr, FEC_FLAG_LIBRARY_STREAM);
     std::memcpy(b0c, b0, 8);
     std::memcpy(b1c, b1, 8);
     const gf* inpkts[3] = {b3, b4, b2};
     gf* outpkts[2] = {b0, b1};
     unsigned indexes[3] = {3, 4, 2};
-    if (st == FEC_OK) st = fec_decode_ex(f, inpkts, outpkts, indexes, 8, nullptr, 0);
+    if (st == FEC_OK) st = fec_decode_ex(f, inpkts, outpkts, indexes, 8, nullptr, FEC_FLAG_LIBRARY_STREAM);
     if (st != FEC_OK) {
         raise_status(st);  // before fec_free, which resets the thread's status
         fec_free(f);
