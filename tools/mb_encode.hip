@@ -1,0 +1,120 @@
+// mb_encode.hip -- microbenchmark of the matrix-apply kernels on one GPU.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_encode.hip -o tools/mb_encode.exe
+// Run:   ./tools/mb_encode.exe [stripe_bytes]
+//
+// 1. A copy-shaped ceiling kernel that moves the K=3/M=10 encode's bytes
+//    (3 16-byte loads, 7 16-byte stores per lane) with trivial arithmetic.
+// 2. The production dispatcher (kernels.hip, included in this TU) over
+//    (k, r) shapes, 16-byte-aligned vs misaligned block bases, and grid caps.
+// Bandwidth = algorithmic bytes (k + r) * block size / kernel time.
+#include "../zfec_amd/csrc/kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace zfec_hip;
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+namespace {
+
+template <int K, int R, bool NT>
+__global__ __launch_bounds__(256) void copy_like(const MatJob job) {
+    const uint32_t n = static_cast<uint32_t>(job.sz / 16);
+    for (uint32_t c = blockIdx.x * 256 + threadIdx.x; c < n; c += gridDim.x * 256) {
+        const uint64_t off = uint64_t(c) * 16;
+        u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc ^= load16(job.in[j] + off);
+#pragma unroll
+        for (int r = 0; r < R; ++r) store16_out<NT>(job.out[r] + off, acc ^ uint32_t(r));
+    }
+}
+
+template <class F>
+float time_ms(F&& launch, int iters) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < iters; ++i) launch();
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return ms / iters;
+}
+
+MatJob make_job(uint8_t* in, uint8_t* out, int k, int r, size_t sz, size_t stride) {
+    MatJob j;
+    memset(&j, 0, sizeof j);
+    j.sz = sz;
+    j.nstripes = 1;
+    j.k = k;
+    j.r = r;
+    for (int i = 0; i < k; ++i) j.in[i] = in + i * stride;
+    for (int i = 0; i < r; ++i) j.out[i] = out + i * stride;
+    for (int i = 0; i < k * r; ++i) j.coef[i] = uint8_t(i * 37 + 11);
+    return j;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const size_t S = argc > 1 ? strtoull(argv[1], nullptr, 0) : (size_t(64) << 20);
+    std::call_once(g_dispatch_once, init_dispatch);
+    {  // copy-shaped ceiling for K=3/M=10
+        const size_t sz = (S / 3 + 255) / 256 * 256;
+        uint8_t *in, *out;
+        CK(hipMalloc(&in, 3 * sz));
+        CK(hipMalloc(&out, 7 * sz));
+        CK(hipMemset(in, 0x5a, 3 * sz));
+        MatJob j = make_job(in, out, 3, 7, sz, sz);
+        for (int nt = 0; nt < 2; ++nt) {
+            const size_t grid = (sz / 16 + 255) / 256;
+            auto fn = nt ? copy_like<3, 7, true> : copy_like<3, 7, false>;
+            float ms = time_ms([&] { hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, 0, j); }, 20);
+            printf("copy_like k=3 r=7 nt=%d                         %8.4f ms  hbm %7.1f GB/s\n", nt, ms,
+                   10.0 * sz / (ms * 1e-3) / 1e9);
+        }
+        CK(hipFree(in));
+        CK(hipFree(out));
+    }
+    const int shapes[][2] = {{3, 7}, {3, 3}, {10, 6}, {10, 4}, {20, 40}, {20, 20}, {16, 16}, {32, 32}, {5, 8}};
+    for (auto& sh : shapes) {
+        const int k = sh[0], r = sh[1];
+        const size_t bsz = (S / k + 255) / 256 * 256;
+        for (int mis : {0, 6}) {
+            const size_t stride = bsz + mis;
+            uint8_t *xin, *xout;
+            CK(hipMalloc(&xin, k * stride + 256));
+            CK(hipMalloc(&xout, r * stride + 256));
+            CK(hipMemset(xin, 0x5a, k * stride + 256));
+            for (int gm : {1, 4, 16}) {
+                g_grid_mult = gm;
+                MatJob j = make_job(xin, xout, k, r, bsz, stride);
+                float ms = time_ms([&] { CK(launch_matapply(j, 0)); }, 20);
+                const double by = double(k + r) * bsz;
+                printf("k=%2d r=%2d mis=%d gm=%2d %-14s %8.4f ms  hbm %7.1f GB/s  input %7.1f GB/s\n", k, r, mis, gm,
+                       matapply_variant_name(k, r, false), ms, by / (ms * 1e-3) / 1e9,
+                       double(k) * bsz / (ms * 1e-3) / 1e9);
+            }
+            CK(hipFree(xin));
+            CK(hipFree(xout));
+        }
+    }
+    return 0;
+}

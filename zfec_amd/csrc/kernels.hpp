@@ -30,11 +30,16 @@ struct alignas(16) MatJob {
     uint32_t cps;          // 16-byte chunks per stripe = ceil(sz / 16)
     uint32_t gs_c, gs_s;   // grid stride expressed as (chunks, stripes): stride = gs_s*cps + gs_c
     uint32_t accumulate;   // 1: out ^= result (continuation pass for k > kMaxIn)
-    uint32_t pad_;
+    uint32_t tables;       // set by launch_matapply: 1 = tab[] holds the per-coefficient tables
     const uint8_t* in[kMaxIn];
     uint8_t* out[kMaxOut];
-    uint8_t coef[kMaxCoef];  // r x k, row-major
+    union {
+        uint8_t coef[kMaxCoef];          // r x k coefficients, row-major (filled by the caller)
+        uint32_t tab[kMaxCoef / 4];      // or their v_perm tables, 5 dwords each (filled by launch_matapply)
+    };
 };
+
+constexpr int kMaxKernargTables = kMaxCoef / 4 / 5;  // 76 coefficients
 
 // Enqueue one launch on `stream`.  Validates shapes against the kernel's
 // compile-time limits before launching (returns hipErrorInvalidValue
