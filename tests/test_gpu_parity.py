@@ -320,3 +320,38 @@ def test_config3_256mib_roundtrip():
     lo, hi = sz // 2, sz // 2 + 100000
     par = torch.stack(out[k:])[:, lo:hi].cpu().numpy()
     assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all()
+
+
+# ---- the reference's own binding on top of the engine ---------------------------
+
+def _dropin_module():
+    import glob
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = glob.glob(os.path.join(root, "oracle", "_ref", "dropin", "_fec*.so"))
+    if not paths:
+        pytest.skip("oracle/_ref/dropin not built (needs /root/reference at build time)")
+    spec = importlib.util.spec_from_file_location("zfec_dropin._fec", paths[0])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_reference_binding_dropin(golden):
+    """zfec/_fecmodule.c compiled unmodified against libzfec_hip.so (oracle/Makefile
+    `dropin`): the reference's own C self-test and Python API run on the GPU
+    engine and reproduce the golden vectors."""
+    ref_api = _dropin_module()
+    assert ref_api.test_from_agl()
+    meta, arrays = golden
+    for ci, c in enumerate(meta["vectors"]):
+        k, m, sz = c["k"], c["m"], c["sz"]
+        inp = arrays["vec%d_in" % ci]
+        allb = arrays["vec%d_all" % ci]
+        out = ref_api.Encoder(k, m).encode(blocks_of(inp))
+        assert [bytes(x) for x in out] == [allb[i].tobytes() for i in range(m)], c
+        nums = c["decode_nums"][0]
+        dec = ref_api.Decoder(k, m).decode([allb[n].tobytes() for n in nums], nums)
+        assert b"".join(bytes(x) for x in dec) == inp.tobytes()

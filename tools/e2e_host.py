@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""End-to-end (host memory -> GPU -> host memory) K=3/M=10 encode and decode
+of one 64 MiB stripe, the path filefec/cmdline_zfec would take.
+
+Strategies timed (GB/s of stripe input bytes, 1e9):
+  bytes_api      zfec_amd.Encoder.encode(list of bytes) -> list of bytes
+                 (pageable host buffers; the library stages them)
+  pinned_api     the same C-ABI call with pinned (hipHostMalloc'd) host buffers,
+                 e.g. a reader that reads file/socket data straight into pinned
+                 memory: the library DMAs them in chunks, overlapping H2D,
+                 kernel and D2H
+  h2d/d2h        raw pinned hipMemcpy rates for reference
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import zfec_amd  # noqa: E402
+from zfec_amd import capi  # noqa: E402
+
+
+def gbps(nbytes, s):
+    return round(nbytes / s / 1e9, 2)
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def main():
+    k, m, S = 3, 10, 64 << 20
+    sz = -(-S // k)
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    blocks = [data[i].tobytes() for i in range(k)]
+    res = {"stripe_bytes": k * sz, "k": k, "m": m}
+
+    enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+    out = enc.encode(blocks)
+    t = timeit(lambda: enc.encode(blocks), 5)
+    res["bytes_api_encode_GBps"] = gbps(k * sz, t)
+    t = timeit(lambda: dec.decode(out[3:6], [3, 4, 5]), 5)
+    res["bytes_api_decode_GBps"] = gbps(k * sz, t)
+    assert dec.decode(out[3:6], [3, 4, 5]) == blocks
+
+    # pinned host buffers through the C-ABI
+    pin_in = torch.from_numpy(data.copy()).pin_memory()
+    pin_out = torch.empty((m - k, sz), dtype=torch.uint8).pin_memory()
+    pin_rec = torch.empty((k, sz), dtype=torch.uint8).pin_memory()
+    code = capi.Code(k, m)
+    ins = [pin_in[i].data_ptr() for i in range(k)]
+    outs = [pin_out[i].data_ptr() for i in range(m - k)]
+
+    def enc_pinned():
+        code.encode_ptrs(ins, outs, list(range(k, m)), sz, flags=capi.FEC_FLAG_LIBRARY_STREAM)
+
+    t = timeit(enc_pinned, 5)
+    res["pinned_api_encode_GBps"] = gbps(k * sz, t)
+    assert b"".join(pin_out[i].numpy().tobytes() for i in range(m - k)) == b"".join(out[k:])
+    rec = [pin_rec[i].data_ptr() for i in range(k)]
+
+    def dec_pinned():
+        code.decode_ptrs([pin_out[i].data_ptr() for i in range(3)], rec, [3, 4, 5], sz,
+                         flags=capi.FEC_FLAG_LIBRARY_STREAM)
+
+    t = timeit(dec_pinned, 5)
+    res["pinned_api_decode_GBps"] = gbps(k * sz, t)
+    assert np.array_equal(pin_rec.numpy(), data)
+
+    # raw copy rates
+    dev = torch.empty((k, sz), dtype=torch.uint8, device="cuda")
+    t = timeit(lambda: dev.copy_(pin_in, non_blocking=True), 5)
+    res["raw_h2d_pinned_GBps"] = gbps(k * sz, t)
+    t = timeit(lambda: pin_in.copy_(dev, non_blocking=True), 5)
+    res["raw_d2h_pinned_GBps"] = gbps(k * sz, t)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -56,8 +56,13 @@ bool valid_code(const fec_t* c) { return c && c->enc_matrix && c->magic == magic
 
 // ---- per-thread, per-device staging -----------------------------------------
 
+constexpr int kSlots = 3;  // pipeline depth of the host path (H2D | kernel | D2H)
+
 struct DevCtx {
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // library stream: kernels of the host path, sync calls
+    hipStream_t h2d = nullptr;     // host -> device copies of the pipeline
+    hipStream_t d2h = nullptr;     // device -> host copies of the pipeline
+    hipEvent_t ev_in[kSlots] = {}, ev_cmp[kSlots] = {}, ev_out[kSlots] = {}, ev_start = nullptr;
     void* dbuf = nullptr;
     size_t dcap = 0;
     void* hbuf = nullptr;  // pinned
@@ -73,6 +78,14 @@ struct ThreadCtx {
             if (hipSetDevice(kv.first) != hipSuccess) continue;
             DevCtx& d = kv.second;
             if (d.stream) (void)hipStreamDestroy(d.stream);
+            if (d.h2d) (void)hipStreamDestroy(d.h2d);
+            if (d.d2h) (void)hipStreamDestroy(d.d2h);
+            for (int i = 0; i < kSlots; ++i) {
+                if (d.ev_in[i]) (void)hipEventDestroy(d.ev_in[i]);
+                if (d.ev_cmp[i]) (void)hipEventDestroy(d.ev_cmp[i]);
+                if (d.ev_out[i]) (void)hipEventDestroy(d.ev_out[i]);
+            }
+            if (d.ev_start) (void)hipEventDestroy(d.ev_start);
             if (d.dbuf) (void)hipFree(d.dbuf);
             if (d.hbuf) (void)hipHostFree(d.hbuf);
             (void)hipSetDevice(cur);
@@ -89,6 +102,22 @@ int dev_ctx(int device, DevCtx** out) {
         if (e != hipSuccess) return hip_fail(e, "hipStreamCreateWithFlags");
     }
     *out = &d;
+    return FEC_OK;
+}
+
+// Streams and events of the host-path pipeline, created on first use.
+int pipeline_ctx(DevCtx& d) {
+    if (d.h2d) return FEC_OK;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&d.h2d, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&d.ev_start, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "pipeline streams");
+    for (int i = 0; i < kSlots; ++i)
+        if ((e = hipEventCreateWithFlags(&d.ev_in[i], hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&d.ev_cmp[i], hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&d.ev_out[i], hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "pipeline events");
     return FEC_OK;
 }
 
@@ -122,15 +151,19 @@ int ensure_hbuf(DevCtx& d, size_t bytes) {
     return FEC_OK;
 }
 
-// Device id of a device-accessible allocation, or -1 for host memory.
-int pointer_device(const void* p) {
+// Device id of a device-accessible allocation, or -1 for host memory; *pinned
+// tells page-locked host memory (hipHostMalloc / hipHostRegister, torch
+// pin_memory) -- DMA-able in place -- from pageable memory.
+int pointer_device(const void* p, bool* pinned = nullptr) {
     hipPointerAttribute_t a;
+    if (pinned) *pinned = false;
     hipError_t e = hipPointerGetAttributes(&a, p);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return -1;
     }
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return a.device;
+    if (pinned) *pinned = a.type == hipMemoryTypeHost;
     return -1;
 }
 
@@ -205,6 +238,7 @@ struct Marshal {
     std::vector<const uint8_t*> din;
     std::vector<uint8_t*> dout;
     std::vector<int> in_host, out_host;  // indices of host-memory blocks
+    bool all_pinned = true;              // every host block is page-locked
 };
 
 // Classify pointers and pick the device.  All device pointers must live on one device.
@@ -214,9 +248,11 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
     int dev = -1;
     auto visit = [&](const void* p, bool is_in, size_t idx) -> int {
         if (!p) return set_status(FEC_EINVAL, "%s block %zu is NULL", is_in ? "input" : "output", idx);
-        const int d = pointer_device(p);
+        bool pinned = false;
+        const int d = pointer_device(p, &pinned);
         if (d < 0) {
             (is_in ? m.in_host : m.out_host).push_back(static_cast<int>(idx));
+            m.all_pinned = m.all_pinned && pinned;
         } else if (dev < 0) {
             dev = d;
         } else if (d != dev) {
@@ -234,13 +270,100 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
 }
 
 // Host blocks of up to this many bytes in total go through one pinned bounce
-// buffer (one H2D / D2H each way); larger ones are copied block by block.
-constexpr size_t kPackLimit = size_t(8) << 20;
+// buffer (one H2D / D2H each way); larger ones stream through the pipeline.
+constexpr size_t kPackLimit = size_t(4) << 20;
+// Bytes of each block per pipeline chunk.
+constexpr size_t kPipeChunk = size_t(2) << 20;
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Run `coef` (r x k) over in -> out, staging host blocks.  Synchronous unless
-// FEC_FLAG_ASYNC and every block is device memory.
+// Pins pageable host ranges for the duration of one call (RAII), so the
+// pipeline can DMA them in place; ZFEC_HIP_REGISTER=0 disables it (the copies
+// then go through HIP's own staging of pageable memory).
+struct HostPins {
+    std::vector<void*> pinned;
+    ~HostPins() {
+        for (void* p : pinned) (void)hipHostUnregister(p);
+    }
+    void pin(const void* p, size_t n) {
+        if (hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault) == hipSuccess)
+            pinned.push_back(const_cast<void*>(p));
+        else
+            (void)hipGetLastError();  // fall back to pageable copies
+    }
+};
+
+bool register_pageable() {
+    static const bool on = [] {
+        const char* e = getenv("ZFEC_HIP_REGISTER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Large host-memory call: the byte range is cut into chunks of kPipeChunk;
+// chunk c's inputs go H2D on d.h2d, its kernel runs on d.stream, its outputs
+// go D2H on d.d2h, with kSlots device staging slots in flight, so copies in
+// both directions overlap each other and the kernels.  Device-resident blocks
+// are read / written in place.
+int run_pipeline(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out,
+                 size_t sz, Marshal& m, hipStream_t user) {
+    if (pipeline_ctx(d)) return t_status;
+    HostPins pins;
+    if (!m.all_pinned && register_pageable()) {
+        for (int i : m.in_host) pins.pin(in[i], sz);
+        for (int i : m.out_host) pins.pin(out[i], sz);
+    }
+    const size_t C = kPipeChunk;
+    const size_t nin = m.in_host.size(), nout = m.out_host.size();
+    const size_t slot_bytes = C * (nin + nout);
+    if (ensure_dbuf(d, slot_bytes * kSlots)) return t_status;
+    hipError_t e;
+    // order after the caller's prior work on `user` (device inputs may be produced there)
+    if ((e = hipEventRecord(d.ev_start, user)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipStreamWaitEvent(d.h2d, d.ev_start, 0)) != hipSuccess ||
+        (e = hipStreamWaitEvent(d.stream, d.ev_start, 0)) != hipSuccess)
+        return hip_fail(e, "hipStreamWaitEvent");
+    std::vector<const uint8_t*> cin(k);
+    std::vector<uint8_t*> cout(r);
+    const size_t nchunks = (sz + C - 1) / C;
+    for (size_t c = 0; c < nchunks; ++c) {
+        const int s = static_cast<int>(c % kSlots);
+        const size_t off = c * C, len = std::min(C, sz - off);
+        uint8_t* base = static_cast<uint8_t*>(d.dbuf) + s * slot_bytes;
+        if (c >= static_cast<size_t>(kSlots)) {  // slot reuse: its previous outputs have left
+            if ((e = hipStreamWaitEvent(d.h2d, d.ev_out[s], 0)) != hipSuccess) return hip_fail(e, "wait");
+            if ((e = hipStreamWaitEvent(d.stream, d.ev_out[s], 0)) != hipSuccess) return hip_fail(e, "wait");
+        }
+        for (unsigned j = 0; j < k; ++j) cin[j] = in[j] + off;
+        for (unsigned i = 0; i < r; ++i) cout[i] = out[i] + off;
+        for (size_t q = 0; q < nin; ++q) {
+            uint8_t* dst = base + q * C;
+            if ((e = hipMemcpyAsync(dst, in[m.in_host[q]] + off, len, hipMemcpyHostToDevice, d.h2d)) != hipSuccess)
+                return hip_fail(e, "hipMemcpyAsync H2D");
+            cin[m.in_host[q]] = dst;
+        }
+        for (size_t q = 0; q < nout; ++q) cout[m.out_host[q]] = base + (nin + q) * C;
+        if ((e = hipEventRecord(d.ev_in[s], d.h2d)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+        if ((e = hipStreamWaitEvent(d.stream, d.ev_in[s], 0)) != hipSuccess) return hip_fail(e, "wait");
+        if (apply_matrix(coef, k, r, cin.data(), cout.data(), len, 1, 0, 0, d.stream)) return t_status;
+        if ((e = hipEventRecord(d.ev_cmp[s], d.stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+        if ((e = hipStreamWaitEvent(d.d2h, d.ev_cmp[s], 0)) != hipSuccess) return hip_fail(e, "wait");
+        for (size_t q = 0; q < nout; ++q)
+            if ((e = hipMemcpyAsync(out[m.out_host[q]] + off, base + (nin + q) * C, len, hipMemcpyDeviceToHost,
+                                    d.d2h)) != hipSuccess)
+                return hip_fail(e, "hipMemcpyAsync D2H");
+        if ((e = hipEventRecord(d.ev_out[s], d.d2h)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    }
+    if ((e = hipStreamSynchronize(d.d2h)) != hipSuccess || (e = hipStreamSynchronize(d.stream)) != hipSuccess)
+        return hip_fail(e, "hipStreamSynchronize");
+    return set_status(FEC_OK);
+}
+
+// Run `coef` (r x k) over in -> out.  Device blocks are used in place; host
+// blocks are staged (small calls: one pinned bounce buffer each way; large
+// calls: the chunked pipeline).  Synchronous unless FEC_FLAG_ASYNC and every
+// block is device memory.
 int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out, size_t sz,
                void* stream_arg, unsigned flags) {
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
@@ -250,61 +373,39 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     DevCtx* d = nullptr;
     if (dev_ctx(m.device, &d)) return t_status;
     hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream_arg);
-    const bool any_host = !m.in_host.empty() || !m.out_host.empty();
     if (sz == 0 || r == 0) return set_status(FEC_OK);
+    const size_t nhost = m.in_host.size() + m.out_host.size();
+    hipError_t e;
+    if (nhost == 0) {
+        if (apply_matrix(coef, k, r, in, out, sz, 1, 0, 0, st)) return t_status;
+        if (!(flags & FEC_FLAG_ASYNC) && (e = hipStreamSynchronize(st)) != hipSuccess)
+            return hip_fail(e, "hipStreamSynchronize");
+        return set_status(FEC_OK);
+    }
+    if (sz * nhost > kPackLimit) return run_pipeline(*d, coef, k, r, in, out, sz, m, st);
 
+    // small call: pack the host inputs into one pinned buffer, one H2D, the
+    // kernel, one D2H of the host outputs, unpack.
     m.din.assign(in, in + k);
     m.dout.assign(out, out + r);
     const size_t slot = align_up(sz, 256);
-    const size_t nhost = m.in_host.size() + m.out_host.size();
-    hipError_t e;
-    if (nhost) {
-        if (ensure_dbuf(*d, slot * nhost)) return t_status;
-        uint8_t* base = static_cast<uint8_t*>(d->dbuf);
-        size_t si = 0;
-        for (int i : m.in_host) m.din[i] = base + slot * si++;
-        for (int i : m.out_host) m.dout[i] = base + slot * si++;
-        const bool pack = sz * nhost <= kPackLimit;
-        if (!m.in_host.empty()) {
-            if (pack) {
-                if (ensure_hbuf(*d, slot * m.in_host.size())) return t_status;
-                // the previous call on this thread has synchronised, so hbuf is free
-                uint8_t* hb = static_cast<uint8_t*>(d->hbuf);
-                for (size_t q = 0; q < m.in_host.size(); ++q) std::memcpy(hb + slot * q, in[m.in_host[q]], sz);
-                e = hipMemcpyAsync(base, hb, slot * m.in_host.size(), hipMemcpyHostToDevice, st);
-                if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
-            } else {
-                for (size_t q = 0; q < m.in_host.size(); ++q) {
-                    e = hipMemcpyAsync(base + slot * q, in[m.in_host[q]], sz, hipMemcpyHostToDevice, st);
-                    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
-                }
-            }
-        }
+    const size_t nin = m.in_host.size(), nout = m.out_host.size();
+    if (ensure_dbuf(*d, slot * nhost) || ensure_hbuf(*d, slot * std::max(nin, nout))) return t_status;
+    uint8_t* base = static_cast<uint8_t*>(d->dbuf);
+    uint8_t* hb = static_cast<uint8_t*>(d->hbuf);  // free: the previous call on this thread synchronised
+    for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = base + slot * q;
+    for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = base + slot * (nin + q);
+    if (nin) {
+        for (size_t q = 0; q < nin; ++q) std::memcpy(hb + slot * q, in[m.in_host[q]], sz);
+        if ((e = hipMemcpyAsync(base, hb, slot * nin, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync H2D");
     }
     if (apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st)) return t_status;
-    if (!m.out_host.empty()) {
-        const size_t nin_h = m.in_host.size();
-        uint8_t* obase = static_cast<uint8_t*>(d->dbuf) + slot * nin_h;
-        const bool pack = sz * nhost <= kPackLimit;
-        if (pack) {
-            if (ensure_hbuf(*d, slot * std::max(m.out_host.size(), nin_h))) return t_status;
-            e = hipMemcpyAsync(d->hbuf, obase, slot * m.out_host.size(), hipMemcpyDeviceToHost, st);
-            if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
-            e = hipStreamSynchronize(st);
-            if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-            const uint8_t* hb = static_cast<const uint8_t*>(d->hbuf);
-            for (size_t q = 0; q < m.out_host.size(); ++q) std::memcpy(out[m.out_host[q]], hb + slot * q, sz);
-        } else {
-            for (size_t q = 0; q < m.out_host.size(); ++q) {
-                e = hipMemcpyAsync(out[m.out_host[q]], obase + slot * q, sz, hipMemcpyDeviceToHost, st);
-                if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync D2H");
-            }
-        }
-    }
-    if (any_host || !(flags & FEC_FLAG_ASYNC)) {
-        e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    }
+    if (nout &&
+        (e = hipMemcpyAsync(hb, base + slot * nin, slot * nout, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync D2H");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    for (size_t q = 0; q < nout; ++q) std::memcpy(out[m.out_host[q]], hb + slot * q, sz);
     return set_status(FEC_OK);
 }
 
