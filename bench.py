@@ -2,26 +2,32 @@
 """bench.py -- device-resident Reed-Solomon encode+decode throughput on MI355X.
 
 Metric (BASELINE.json): "encode+decode GB/s (device-resident input) at K/M;
-% of HBM roofline".  Workload (BASELINE.json configs[1]): K=3, M=10, one
-64 MiB stripe per GPU (block size sz = ceil(64 MiB / 3) = 22,369,622 B).
+% of HBM roofline".  Default workload = BASELINE.json configs[1]: K=3, M=10,
+one 64 MiB stripe per GPU (block size sz = ceil(64 MiB / 3) = 22,369,622 B).
+Other configs (--workload cfg3|cfg4|cfg5) are the parity-test cases, timed
+the same way for DESIGN.md.
 
-One step = encode the stripe (3 primaries -> 7 secondaries, one launch) +
-secondary-only decode (blocks 3,4,5 -> primaries 0,1,2, one launch), both
-through the C-ABI (fec_encode_batch / fec_decode_batch) on torch's current
-stream, inputs resident in HBM.  value = (encode input + decode input bytes)
-= 2*k*sz per step per GPU, summed over GPUs, / wall time of the K timed steps
-(max over ranks), in GB/s (1e9).
+One step = encode every stripe of the workload (k primaries -> m-k
+secondaries, one launch of fec_encode_batch) + decode them back from
+secondary blocks (one launch of fec_decode_batch), inputs resident in HBM.
+value = (encode input + decode input bytes) = 2 * k * sz * stripes per step,
+summed over GPUs, / wall time of the K timed steps (max over ranks), GB/s
+(1e9).  The step's two launches are captured once into a HIP graph and
+replayed per step (--eager: plain launches).
 
-Multi-GPU (torchrun, one rank per GPU): each rank encodes/decodes its own
-stripe -- stripes are independent, no data-path collective (weak scaling);
-the only collectives are the timing barrier and the max-over-ranks reduce.
+Multi-GPU (torchrun, one rank per GPU): stripes are independent, so ranks
+never exchange data.  cfg2/cfg3: each rank owns its own stripe (weak
+scaling).  cfg4/cfg5: the fixed batch is split by zfec_amd.shard.shard_range
+(strong scaling).  The only collectives are the timing barrier and the
+max/sum reductions.
 
-Also reported: the dominant kernel's roofline (encode: (k+r)*sz algorithmic
-HBM bytes per launch / mean launch time from HIP events on the launch
-stream), the decode kernel's, a batched 1 MiB-stripe encode (the north-star
-target shape), and a bounded CPU baseline (rank 0, N=1) of the reference's
-own C code (oracle/_ref, kind "reference") or the oracle restatement (kind
-"port").
+Also reported: the dominant kernel's roofline (encode: (k+r)*sz*stripes
+algorithmic HBM bytes per launch / mean launch time, 20 back-to-back
+launches between HIP events on the launch stream; PMC traffic from
+profiles/pmc_summary.json), the decode kernel's, a batched 1 MiB-stripe
+encode (the north-star shape), and a bounded CPU baseline (rank 0, N=1) of
+the reference's own C code (oracle/_ref, kind "reference") or the oracle
+restatement (kind "port").
 """
 import argparse
 import json
@@ -37,11 +43,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from zfec_amd import capi  # noqa: E402
+from zfec_amd.shard import shard_range  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "encode+decode GB/s (device-resident input) at K/M; % of HBM roofline"
 
-K, M = 3, 10
-STRIPE = 64 << 20
+# name: (k, m, stripe bytes, stripes, scaling)
+WORKLOADS = {
+    "cfg2": (3, 10, 64 << 20, 1, "weak"),
+    "cfg3": (10, 16, 256 << 20, 1, "weak"),
+    "cfg4": (20, 60, 1 << 20, 1024, "strong"),
+    "cfg5": (3, 10, 4 << 10, 1000000, "strong"),
+}
 
 
 def parse():
@@ -49,13 +62,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip the 1 MiB-stripe batched leg")
+    p.add_argument("--eager", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     return p.parse_args()
 
 
-def dist_setup(args):
+def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -64,9 +79,9 @@ def dist_setup(args):
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        return dist, rank, world, local
+        return dist, rank, world
     torch.cuda.set_device(0)
-    return None, 0, 1, 0
+    return None, 0, 1
 
 
 def barrier(dist):
@@ -74,37 +89,42 @@ def barrier(dist):
         dist.barrier()
 
 
-def max_over_ranks(dist, x):
+def reduce(dist, x, op):
     if dist is None:
         return x
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=op)
     return float(t.item())
 
 
-def sum_over_ranks(dist, x):
-    if dist is None:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def align_up(x, a):
+    return (x + a - 1) // a * a
 
 
-def pmc_traffic():
+def place(nums, k):
+    """Slot order with primary i at slot i (zfec/_fecmodule.c:482-493)."""
+    slots = [None] * k
+    sec = iter([n for n in nums if n >= k])
+    for n in nums:
+        if n < k:
+            slots[n] = n
+    return [s if s is not None else next(sec) for s in slots]
+
+
+def pmc_traffic(workload):
     """Per-launch HBM bytes of the encode kernel from the committed PMC summary
-    (profiles/pmc_summary.json, made by tools/pmc.sh + tools/pmc_summary.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    (profiles/pmc_summary.json, made by tools/profile_round.sh + tools/pmc_summary.py)."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
             d = json.load(f)
-        return d.get("encode_cfg2", {}).get("hbm_bytes_per_launch")
+        return d.get("encode_" + workload, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(seconds, sz):
+def cpu_baseline(seconds, k, m, sz):
     """Bounded CPU sample of the same workload (encode + secondary-only decode
-    of one K=3/M=10 stripe of 3*sz bytes per step), one stripe per thread."""
+    of one stripe of k*sz bytes per step), one stripe per thread."""
     from oracle import oracle
 
     ref = oracle.ref_module()
@@ -114,28 +134,28 @@ def cpu_baseline(seconds, sz):
         threads = os.cpu_count() or 1
     threads = max(1, min(16, threads))
     rng = np.random.default_rng(7)
-    proto = [rng.integers(0, 256, size=sz, dtype=np.uint8).tobytes() for _ in range(K)]
+    proto = [rng.integers(0, 256, size=sz, dtype=np.uint8).tobytes() for _ in range(k)]
     counts = [0] * threads
     stop = threading.Event()
-
+    sec = list(range(k, 2 * k))
     if ref is not None:
         kind = "reference"
 
         def work(t):
-            enc, dec = ref.Encoder(K, M), ref.Decoder(K, M)
+            enc, dec = ref.Encoder(k, m), ref.Decoder(k, m)
             blocks = [bytes(b) for b in proto]
             while not stop.is_set():
                 out = enc.encode(blocks)
-                dec.decode(out[K:2 * K], list(range(K, 2 * K)))
+                dec.decode(out[k:2 * k], sec)
                 counts[t] += 1
     else:
         kind = "port"
-        data = np.frombuffer(b"".join(proto), dtype=np.uint8).reshape(K, sz)
+        data = np.frombuffer(b"".join(proto), dtype=np.uint8).reshape(k, sz)
 
         def work(t):
             while not stop.is_set():
-                par = oracle.encode(K, M, data)
-                oracle.decode(K, M, par[:K], list(range(K, 2 * K)))
+                par = oracle.encode(k, m, data)
+                oracle.decode(k, m, par[:k], sec)
                 counts[t] += 1
 
     ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
@@ -148,78 +168,97 @@ def cpu_baseline(seconds, sz):
         th.join()
     el = time.perf_counter() - t0
     steps = sum(counts)
-    gbps = steps * 2 * K * sz / el / 1e9
-    return {"value": round(gbps, 4), "unit": "GB/s", "cores": threads, "kind": kind,
-            "sample": "%d steps (encode+secondary-only decode of a K=3/M=10 %d-byte stripe) in %.1f s, "
-                      "one stripe per thread; %s" % (
-                          steps, K * sz, el,
+    return {"value": round(steps * 2 * k * sz / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": kind,
+            "sample": "%d steps (encode + secondary-only decode of a K=%d/M=%d %d-byte stripe) in %.1f s, one "
+                      "stripe per thread; %s" % (
+                          steps, k, m, k * sz, el,
                           "reference zfec/fec.c+_fecmodule.c compiled by oracle/Makefile (-O2 -march=x86-64-v2)"
                           if kind == "reference" else "oracle/fec_oracle.c restatement")}
 
 
-def align_up(x, a):
-    return (x + a - 1) // a * a
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=True):
+    """Encode + decode `ns` stripes per step; returns timings.
 
-
-def run_stripe_bench(code, k, m, sz, steps, warmup, dist):
-    """Returns (elapsed_s, enc_ms_mean, dec_ms_mean) over `steps` timed steps.
-
-    HBM layout: each stripe is a [block][row_stride] array whose row stride is
-    sz rounded up to 256 bytes, so every block starts 256-byte aligned (the
-    blocks of the reference's API are separate buffers, i.e. aligned too)."""
+    HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
+    to 256 bytes, so every block starts 256-byte aligned (the reference's API
+    takes separate buffers per block, which are aligned too)."""
     r = m - k
     ld = align_up(sz, 256)
-    g = torch.Generator(device="cuda").manual_seed(1234 + k)
-    data = torch.randint(0, 256, (k, ld), dtype=torch.uint8, device="cuda", generator=g)
-    par = torch.empty((r, ld), dtype=torch.uint8, device="cuda")
-    rec = torch.empty((k, ld), dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
+    gen = torch.Generator(device="cuda").manual_seed(1234 + k)
+    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen)
+    par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
+    # decode from the last k blocks (all secondaries when m >= 2k); primaries at their slot
+    slots = place(list(range(m - k, m)), k)
+    nrec = sum(1 for s in slots if s >= k)
+    recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")  # received blocks, slot order
+    rec = torch.empty((ns, nrec, ld), dtype=torch.uint8, device="cuda")
     enc_nums = list(range(k, m))
-    dec_slots = list(range(k, 2 * k))  # blocks 3,4,5: no primaries present
+    code = capi.Code(k, m)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        code.encode_batch(data.data_ptr(), ld, 0, par.data_ptr(), ld, 0, enc_nums, sz, 1, stream=sh)
-        if ev is not None:
-            ev[1].record(stream)
-        code.decode_batch(par.data_ptr(), ld, 0, rec.data_ptr(), ld, 0, dec_slots, sz, 1, stream=sh)
-        if ev is not None:
-            ev[2].record(stream)
+    def enc(sh):
+        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, enc_nums, sz, ns, stream=sh)
 
+    def dec(sh):
+        code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, nrec * ld, slots, sz, ns, stream=sh)
+
+    stream = torch.cuda.current_stream()
+    enc(stream.cuda_stream)
+    for i, s in enumerate(slots):  # stage the received blocks once (not part of a step)
+        recv[:, i].copy_(data[:, s] if s < k else par[:, s - k])
     for _ in range(warmup):
+        enc(stream.cuda_stream)
+        dec(stream.cuda_stream)
+    torch.cuda.synchronize()
+    missing = [i for i in range(k) if slots[i] >= k]
+    assert torch.equal(rec[:, :, :sz], data[:, missing, :sz]), "decode(encode(x)) != x"
+
+    launch = "eager"
+    step = lambda: (enc(stream.cuda_stream), dec(stream.cuda_stream))
+    if use_graph:
+        try:
+            cap = torch.cuda.Stream()
+            graph = torch.cuda.CUDAGraph()
+            cap.wait_stream(stream)
+            with torch.cuda.graph(graph, stream=cap):
+                enc(cap.cuda_stream)
+                dec(cap.cuda_stream)
+            torch.cuda.synchronize()
+            rec.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(rec[:, :, :sz], data[:, missing, :sz]), "graph replay: decode(encode(x)) != x"
+            step = graph.replay
+            launch = "hipGraph (1 replay per step)"
+        except Exception as e:  # capture unsupported: keep eager launches
+            launch = "eager (graph capture failed: %s: %s)" % (type(e).__name__, str(e)[:120])
+    for _ in range(3):
         step()
     torch.cuda.synchronize()
-    # correctness of the timed configuration (size-independent property)
-    assert torch.equal(rec[:, :sz], data[:, :sz]), "decode(encode(x)) != x"
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     barrier(dist)
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for i in range(steps):
-        step(evs[i])
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
     torch.cuda.synchronize()
     barrier(dist)
     el = time.perf_counter() - t0
-    step_enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    step_dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
-    # Per-kernel launch duration for the roofline: the same launches back to
-    # back on the same stream, bracketed by one pair of HIP events (the
-    # in-step brackets above also contain each launch's dispatch latency).
+    # Per-kernel launch duration for the roofline: each kernel launched back to
+    # back on the same stream, bracketed by one pair of HIP events.
     def b2b(fn, n=20):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
         for _ in range(n):
-            fn()
-        e1.record(stream)
+            fn(stream.cuda_stream)
+        b.record(stream)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / n
+        return a.elapsed_time(b) / n
 
-    enc_ms = b2b(lambda: code.encode_batch(data.data_ptr(), ld, 0, par.data_ptr(), ld, 0, enc_nums, sz, 1, stream=sh))
-    dec_ms = b2b(lambda: code.decode_batch(par.data_ptr(), ld, 0, rec.data_ptr(), ld, 0, dec_slots, sz, 1, stream=sh))
-    return el, enc_ms, dec_ms, step_enc_ms, step_dec_ms
+    return {"elapsed_s": el, "gpu_step_ms": e0.elapsed_time(e1) / steps, "launch": launch,
+            "enc_ms": b2b(enc), "dec_ms": b2b(dec), "nrec": nrec, "slots": slots}
 
 
 def run_batched_1mib(steps):
@@ -233,12 +272,17 @@ def run_batched_1mib(steps):
     dst = torch.empty((ns, m - k, ld), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     nums = list(range(k, m))
+
+    def enc():
+        code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, (m - k) * ld, nums, sz, ns,
+                          stream=st.cuda_stream)
+
     for _ in range(3):
-        code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, (m - k) * ld, nums, sz, ns, stream=st.cuda_stream)
+        enc()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(steps):
-        code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, (m - k) * ld, nums, sz, ns, stream=st.cuda_stream)
+        enc()
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
@@ -250,19 +294,30 @@ def run_batched_1mib(steps):
 
 def main():
     args = parse()
-    dist, rank, world, local = dist_setup(args)
-    sz = -(-STRIPE // K)
-    code = capi.Code(K, M)
-    el, enc_ms, dec_ms, step_enc_ms, step_dec_ms = run_stripe_bench(code, K, M, sz, args.steps, args.warmup, dist)
-    el = max_over_ranks(dist, el)
-    total_bytes = sum_over_ranks(dist, float(args.steps * 2 * K * sz))
+    dist, rank, world = dist_setup()
+    k, m, stripe, nstripes, scaling = WORKLOADS[args.workload]
+    r = m - k
+    sz = -(-stripe // k)
+    if scaling == "strong":
+        s0, s1 = shard_range(nstripes, world, rank)
+        ns = s1 - s0
+    else:
+        ns = nstripes
+    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=not args.eager)
+    el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
+    total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
     value = total_bytes / el / 1e9
-    enc_bytes = (K + (M - K)) * sz       # read k blocks, write m-k blocks
-    dec_bytes = (K + K) * sz             # read k blocks, write k recovered
-    enc_ach = enc_bytes / (enc_ms * 1e-3) / 1e9
-    dec_ach = dec_bytes / (dec_ms * 1e-3) / 1e9
+    nrec = t["nrec"]
+    enc_bytes = (k + r) * sz * ns    # read k blocks, write m-k blocks, per stripe
+    dec_bytes = (k + nrec) * sz * ns  # read k blocks, write the recovered ones
+    enc_ach = enc_bytes / (t["enc_ms"] * 1e-3) / 1e9
+    dec_ach = dec_bytes / (t["dec_ms"] * 1e-3) / 1e9
+    desc = {"cfg2": "K=3 M=10, one 64 MiB stripe per GPU",
+            "cfg3": "K=10 M=16, one 256 MiB stripe per GPU",
+            "cfg4": "K=20 M=60, 1 GiB = 1024 x 1 MiB stripes split across GPUs",
+            "cfg5": "K=3 M=10, 1e6 x 4 KiB objects split across GPUs"}[args.workload]
     out = {
-        "metric": "encode+decode GB/s (device-resident input) at K/M; % of HBM roofline",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
@@ -270,29 +325,32 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (torch.randint bytes, resident in HBM)",
-        "config": {"workload": "K=3 M=10, one 64 MiB stripe per GPU: encode (3->7 blocks) + secondary-only "
-                               "decode (blocks 3,4,5 -> 0,1,2)", "k": K, "m": M, "stripe_bytes": STRIPE,
-                   "block_bytes": sz, "block_row_stride": align_up(sz, 256), "parallelism": "stripes sharded across GPUs (dp%d), no collective" % world},
+        "config": {"workload": "%s: encode (%d->%d blocks) + decode from blocks %s" % (desc, k, r, t["slots"]),
+                   "name": args.workload, "k": k, "m": m, "stripe_bytes": stripe, "stripes_per_gpu": ns,
+                   "block_bytes": sz, "block_row_stride": align_up(sz, 256),
+                   "parallelism": "stripes sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": round(enc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(),
-                     "kernel": "matapply_reg<3,7> (encode)", "algorithmic_bytes_per_launch": enc_bytes,
-                     "launch_ms": round(enc_ms, 4), "in_step_event_ms": round(step_enc_ms, 4),
+                     "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),
+                     "kernel": "%s (encode)" % capi.variant_name(k, r), "algorithmic_bytes_per_launch": enc_bytes,
+                     "launch_ms": round(t["enc_ms"], 4),
                      "timing": "20 back-to-back launches between two HIP events on the launch stream"},
         "decode_roofline": {"achieved": round(dec_ach, 1), "frac": round(dec_ach / HBM_PEAK_GBPS, 4),
-                            "kernel": "matapply_reg<3,3> (decode)", "algorithmic_bytes_per_launch": dec_bytes,
-                            "launch_ms": round(dec_ms, 4), "in_step_event_ms": round(step_dec_ms, 4)},
-        "encode_input_GBps": round(K * sz / (enc_ms * 1e-3) / 1e9, 1),
-        "decode_input_GBps": round(K * sz / (dec_ms * 1e-3) / 1e9, 1),
+                            "kernel": "%s (decode)" % capi.variant_name(k, nrec),
+                            "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4)},
+        "launch": t["launch"],
+        "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
+        "encode_input_GBps": round(k * sz * ns / (t["enc_ms"] * 1e-3) / 1e9, 1),
+        "decode_input_GBps": round(k * sz * ns / (t["dec_ms"] * 1e-3) / 1e9, 1),
     }
-    if rank == 0 and not args.no_extra:
+    if rank == 0 and not args.no_extra and args.workload == "cfg2":
         out["batched_1MiB"] = run_batched_1mib(20)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sz)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, k, m, sz)
         except Exception as e:  # the baseline must never sink the GPU measurement
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

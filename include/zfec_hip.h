@@ -132,6 +132,10 @@ int fec_device_count(void);
 /* Library version string. */
 const char* fec_version(void);
 
+/* Name of the kernel variant a launch with k inputs and r outputs uses
+ * (diagnostics and profiling; k <= 32, r <= 48 per launch). */
+const char* fec_kernel_name(unsigned k, unsigned r);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,7 @@ SYMBOLS = [
     ("fec_decode_batch", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _P, _U]),
     ("fec_device_count", ctypes.c_int, []),
     ("fec_version", ctypes.c_char_p, []),
+    ("fec_kernel_name", ctypes.c_char_p, [_U, _U]),
 ]
 
 
@@ -74,6 +75,11 @@ class FecError(RuntimeError):
 def check(status):
     if status != FEC_OK:
         raise FecError("zfec-hip status %d: %s" % (status, lib().fec_last_error_message().decode()))
+
+
+def variant_name(k, r):
+    """Kernel variant used for k inputs and r outputs (fec_kernel_name)."""
+    return lib().fec_kernel_name(k, r).decode()
 
 
 def ptr_array(addrs):

@@ -567,6 +567,11 @@ FEC_API int fec_device_count(void) { return gpu_available(); }
 
 FEC_API const char* fec_version(void) { return "zfec-hip 0.1.0 (gfx950)"; }
 
+FEC_API const char* fec_kernel_name(unsigned k, unsigned r) {
+    if (k == 0 || r == 0 || k > static_cast<unsigned>(kMaxIn) || r > static_cast<unsigned>(kMaxOut)) return "split";
+    return matapply_variant_name(k, r, false);
+}
+
 namespace {
 int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src, size_t sbs, size_t sss, gf* dst,
               size_t dbs, size_t dss, size_t sz, size_t nstripes, void* stream, unsigned flags) {

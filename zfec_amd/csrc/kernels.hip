@@ -346,6 +346,16 @@ struct Variant {
 
 // Register-table variants: k <= 4, r <= 8.
 constexpr int kRegK = 4, kRegR = 8;
+const char* const kRegNames[kRegK + 1][kRegR + 1] = {
+    {},
+    {"", "matapply_reg<1,1>", "matapply_reg<1,2>", "matapply_reg<1,3>", "matapply_reg<1,4>", "matapply_reg<1,5>",
+     "matapply_reg<1,6>", "matapply_reg<1,7>", "matapply_reg<1,8>"},
+    {"", "matapply_reg<2,1>", "matapply_reg<2,2>", "matapply_reg<2,3>", "matapply_reg<2,4>", "matapply_reg<2,5>",
+     "matapply_reg<2,6>", "matapply_reg<2,7>", "matapply_reg<2,8>"},
+    {"", "matapply_reg<3,1>", "matapply_reg<3,2>", "matapply_reg<3,3>", "matapply_reg<3,4>", "matapply_reg<3,5>",
+     "matapply_reg<3,6>", "matapply_reg<3,7>", "matapply_reg<3,8>"},
+    {"", "matapply_reg<4,1>", "matapply_reg<4,2>", "matapply_reg<4,3>", "matapply_reg<4,4>", "matapply_reg<4,5>",
+     "matapply_reg<4,6>", "matapply_reg<4,7>", "matapply_reg<4,8>"}};
 Variant g_reg[kRegK + 1][kRegR + 1];
 Variant g_gen, g_gen_acc, g_gen_tab;
 std::once_flag g_dispatch_once;
@@ -354,7 +364,7 @@ int g_grid_mult = 16;  // grid cap = CUs x resident blocks per CU x g_grid_mult
 
 template <int K, int R>
 void set_reg() {
-    g_reg[K][R] = Variant{matapply_reg<K, R, true>, "matapply_reg", 0, true};
+    g_reg[K][R] = Variant{matapply_reg<K, R, true>, kRegNames[K][R], 0, true};
 }
 
 template <int K>
