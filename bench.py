@@ -12,8 +12,9 @@ secondaries, one launch of fec_encode_batch) + decode them back from
 secondary blocks (one launch of fec_decode_batch), inputs resident in HBM.
 value = (encode input + decode input bytes) = 2 * k * sz * stripes per step,
 summed over GPUs, / wall time of the K timed steps (max over ranks), GB/s
-(1e9).  The step's two launches are captured once into a HIP graph and
-replayed per step (--eager: plain launches).
+(1e9).  The step's two launches are plain stream-ordered launches (--graph:
+capture them once into a HIP graph and replay it per step; on ROCm 7.2 the
+replay measured slower than eager launches).
 
 Multi-GPU (torchrun, one rank per GPU): stripes are independent, so ranks
 never exchange data.  cfg2/cfg3: each rank owns its own stripe (weak
@@ -66,7 +67,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip the 1 MiB-stripe batched leg")
-    p.add_argument("--eager", action="store_true", help="launch eagerly instead of replaying a HIP graph")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
 
 
@@ -166,7 +168,7 @@ def cpu_baseline(seconds, k, m, sz):
     stop.set()
     for th in ths:
         th.join()
-    el = time.perf_counter() - t0
+    el = time.perf_counter() - t0  # threads finish their step in flight; all of it is counted
     steps = sum(counts)
     return {"value": round(steps * 2 * k * sz / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": kind,
             "sample": "%d steps (encode + secondary-only decode of a K=%d/M=%d %d-byte stripe) in %.1f s, one "
@@ -176,7 +178,7 @@ def cpu_baseline(seconds, k, m, sz):
                           if kind == "reference" else "oracle/fec_oracle.c restatement")}
 
 
-def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=True):
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
@@ -303,7 +305,7 @@ def main():
         ns = s1 - s0
     else:
         ns = nstripes
-    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=not args.eager)
+    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
     value = total_bytes / el / 1e9
@@ -350,7 +352,8 @@ def main():
         out["batched_1MiB"] = run_batched_1mib(20)
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, k, m, sz)
+            csz = min(sz, -(-(64 << 20) // k))  # sample stripes of at most 64 MiB (same K/M)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, k, m, csz)
         except Exception as e:  # the baseline must never sink the GPU measurement
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

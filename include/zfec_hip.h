@@ -126,6 +126,13 @@ int fec_decode_batch(const fec_t* code,
                      const unsigned* index, size_t sz, size_t nstripes,
                      void* stream, unsigned flags);
 
+/* Page-locked host memory on the current device's node (hipHostMalloc): host
+ * buffers passed to fec_encode / fec_decode from here are DMA'd in place by
+ * the overlapped H2D / kernel / D2H pipeline (no per-call pinning).  NULL on
+ * failure (status set). */
+void* fec_host_alloc(size_t bytes);
+void fec_host_free(void* p);
+
 /* Number of visible GPUs (0 when none; never aborts). */
 int fec_device_count(void);
 

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 using namespace zfec_hip;
@@ -58,7 +59,8 @@ float time_ms(F&& launch, int iters) {
     return ms / iters;
 }
 
-MatJob make_job(uint8_t* in, uint8_t* out, int k, int r, size_t sz, size_t stride) {
+MatJob make_job(uint8_t* in, uint8_t* out, int k, int r, size_t sz, size_t stride, size_t ostride = 0) {
+    if (!ostride) ostride = stride;
     MatJob j;
     memset(&j, 0, sizeof j);
     j.sz = sz;
@@ -66,7 +68,7 @@ MatJob make_job(uint8_t* in, uint8_t* out, int k, int r, size_t sz, size_t strid
     j.k = k;
     j.r = r;
     for (int i = 0; i < k; ++i) j.in[i] = in + i * stride;
-    for (int i = 0; i < r; ++i) j.out[i] = out + i * stride;
+    for (int i = 0; i < r; ++i) j.out[i] = out + i * ostride;
     for (int i = 0; i < k * r; ++i) j.coef[i] = uint8_t(i * 37 + 11);
     return j;
 }
@@ -93,6 +95,105 @@ int main(int argc, char** argv) {
         CK(hipFree(in));
         CK(hipFree(out));
     }
+    {  // misalignment split: inputs only / outputs only (K=3/M=10 encode)
+        const int k = 3, r = 7;
+        const size_t bsz = (S / k + 255) / 256 * 256;
+        for (int mi : {0, 6}) for (int mo : {0, 6}) {
+            uint8_t *xin, *xout;
+            CK(hipMalloc(&xin, k * (bsz + mi) + 256));
+            CK(hipMalloc(&xout, r * (bsz + mo) + 256));
+            CK(hipMemset(xin, 0x5a, k * (bsz + mi) + 256));
+            g_grid_mult = 16;
+            MatJob j = make_job(xin, xout, k, r, bsz, bsz + mi, bsz + mo);
+            float ms = time_ms([&] { CK(launch_matapply(j, 0)); }, 20);
+            printf("k=3 r=7 mis_in=%d mis_out=%d %8.4f ms  hbm %7.1f GB/s\n", mi, mo, ms, 10.0 * bsz / (ms * 1e-3) / 1e9);
+            CK(hipFree(xin));
+            CK(hipFree(xout));
+        }
+    }
+    if (getenv("MB_AB")) {  // interleaved A/B of store policy: 7 rounds, median (guide §5.4 rule 24)
+        struct V {
+            const char* name;
+            KernelFn fn;
+            int k, r;
+            bool ktab;
+        } vs[] = {
+            {"reg<3,7> nt", matapply_reg<3, 7, true, 1>, 3, 7, true},
+            {"reg<3,7> plain", matapply_reg<3, 7, false, 1>, 3, 7, true},
+            {"reg<3,3> nt", matapply_reg<3, 3, true, 1>, 3, 3, true},
+            {"reg<3,3> plain", matapply_reg<3, 3, false, 1>, 3, 3, true},
+            {"gen<ktab> 10x6 nt", matapply_gen<false, true, true>, 10, 6, true},
+            {"gen<ktab> 10x6 plain", matapply_gen<false, false, true>, 10, 6, true},
+            {"gen 20x40 nt", matapply_gen<false, true, false>, 20, 40, false},
+            {"gen 20x40 plain", matapply_gen<false, false, false>, 20, 40, false},
+        };
+        const int nv = sizeof(vs) / sizeof(vs[0]);
+        std::vector<std::vector<float>> t(nv);
+        std::vector<uint8_t*> ins(nv), outs(nv);
+        std::vector<size_t> bszs(nv);
+        for (int i = 0; i < nv; ++i) {
+            bszs[i] = (S / vs[i].k + 255) / 256 * 256;
+            CK(hipMalloc(&ins[i], vs[i].k * bszs[i]));
+            CK(hipMalloc(&outs[i], vs[i].r * bszs[i]));
+            CK(hipMemset(ins[i], 0x5a, vs[i].k * bszs[i]));
+        }
+        for (int round = 0; round < 7; ++round)
+            for (int i = 0; i < nv; ++i) {
+                Variant* slot = vs[i].k <= kRegK && vs[i].r <= kRegR ? &g_reg[vs[i].k][vs[i].r]
+                                : (vs[i].ktab ? &g_gen_tab : &g_gen);
+                const Variant saved = *slot;
+                *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1};
+                g_grid_mult = 16;
+                MatJob j = make_job(ins[i], outs[i], vs[i].k, vs[i].r, bszs[i], bszs[i]);
+                t[i].push_back(time_ms([&] { MatJob jj = j; CK(launch_matapply(jj, 0)); }, 10));
+                *slot = saved;
+            }
+        for (int i = 0; i < nv; ++i) {
+            std::sort(t[i].begin(), t[i].end());
+            const double by = double(vs[i].k + vs[i].r) * bszs[i];
+            printf("AB %-22s median %8.4f ms (min %8.4f)  hbm %7.1f GB/s\n", vs[i].name, t[i][3], t[i][0],
+                   by / (t[i][3] * 1e-3) / 1e9);
+        }
+        return 0;
+    }
+    {  // kernel variants of the K=3 register path, aligned layout
+        struct V {
+            const char* name;
+            KernelFn fn;
+            int upl;
+            int k, r;
+        } vs[] = {
+            {"reg<3,7> nt U1", matapply_reg<3, 7, true, 1>, 1, 3, 7},
+            {"reg<3,7> nt U2", matapply_reg<3, 7, true, 2>, 2, 3, 7},
+            {"reg<3,7> plain U1", matapply_reg<3, 7, false, 1>, 1, 3, 7},
+            {"reg<3,7> plain U2", matapply_reg<3, 7, false, 2>, 2, 3, 7},
+            {"reg<3,3> nt U1", matapply_reg<3, 3, true, 1>, 1, 3, 3},
+            {"reg<3,3> nt U2", matapply_reg<3, 3, true, 2>, 2, 3, 3},
+            {"reg<3,3> plain U1", matapply_reg<3, 3, false, 1>, 1, 3, 3},
+        };
+        for (auto& v : vs) {
+            const Variant saved = g_reg[v.k][v.r];
+            g_reg[v.k][v.r] = Variant{v.fn, v.name, 0, true, v.upl};
+            const size_t bsz = (S / v.k + 255) / 256 * 256;
+            uint8_t *xin, *xout;
+            CK(hipMalloc(&xin, v.k * bsz));
+            CK(hipMalloc(&xout, v.r * bsz));
+            CK(hipMemset(xin, 0x5a, v.k * bsz));
+            hipFuncAttributes attr;
+            CK(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(v.fn)));
+            for (int gm : {2, 16}) {
+                g_grid_mult = gm;
+                MatJob j = make_job(xin, xout, v.k, v.r, bsz, bsz);
+                float ms = time_ms([&] { CK(launch_matapply(j, 0)); }, 20);
+                printf("variant %-18s vgpr=%3d sgpr=%3d gm=%2d %8.4f ms  hbm %7.1f GB/s\n", v.name, attr.numRegs,
+                       0, gm, ms, double(v.k + v.r) * bsz / (ms * 1e-3) / 1e9);
+            }
+            CK(hipFree(xin));
+            CK(hipFree(xout));
+            g_reg[v.k][v.r] = saved;
+        }
+    }
+    if (getenv("MB_MIS_ONLY")) return 0;
     const int shapes[][2] = {{3, 7}, {3, 3}, {10, 6}, {10, 4}, {20, 40}, {20, 20}, {16, 16}, {32, 32}, {5, 8}};
     for (auto& sh : shapes) {
         const int k = sh[0], r = sh[1];

@@ -34,6 +34,8 @@ SYMBOLS = [
     ("fec_decode_ex", ctypes.c_int, [_P, _PP, _PP, _UP, _SZ, _P, _U]),
     ("fec_encode_batch", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _SZ, _P, _U]),
     ("fec_decode_batch", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _P, _U]),
+    ("fec_host_alloc", _P, [_SZ]),
+    ("fec_host_free", None, [_P]),
     ("fec_device_count", ctypes.c_int, []),
     ("fec_version", ctypes.c_char_p, []),
     ("fec_kernel_name", ctypes.c_char_p, [_U, _U]),

@@ -565,6 +565,26 @@ FEC_API const char* fec_last_error_message(void) { return t_msg; }
 
 FEC_API int fec_device_count(void) { return gpu_available(); }
 
+FEC_API void* fec_host_alloc(size_t bytes) {
+    if (!gpu_available()) {
+        set_status(FEC_ENODEV, "no GPU visible to HIP");
+        return nullptr;
+    }
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_status(FEC_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    set_status(FEC_OK);
+    return p;
+}
+
+FEC_API void fec_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+    set_status(FEC_OK);
+}
+
 FEC_API const char* fec_version(void) { return "zfec-hip 0.1.0 (gfx950)"; }
 
 FEC_API const char* fec_kernel_name(unsigned k, unsigned r) {

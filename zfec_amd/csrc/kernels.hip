@@ -208,7 +208,42 @@ struct UnitIter {
 // kernel arguments (prefetched scalar loads); the compiler keeps the high
 // words in SGPRs and copies the low words to VGPRs once, outside the loop.
 // ---------------------------------------------------------------------------
+// One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.
 template <int K, int R, bool NT>
+__device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
+                                                  uint64_t ob, bool full, uint32_t nb) {
+    Sel sel[4][K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        sel[0][j] = selectors(x[j].x);
+        sel[1][j] = selectors(x[j].y);
+        sel[2][j] = selectors(x[j].z);
+        sel[3][j] = selectors(x[j].w);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32x4 y{gf_dot<K>(T[r], sel[0]), gf_dot<K>(T[r], sel[1]), gf_dot<K>(T[r], sel[2]),
+                      gf_dot<K>(T[r], sel[3])};
+        if (full)
+            store16_out<NT>(job.out[r] + ob, y);
+        else
+            store_tail(job.out[r] + ob, y, nb);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint64_t ib, bool full, uint32_t nb) {
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + ib);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load_tail(job.in[j] + ib, nb);
+    }
+}
+
+// U: units per lane per loop trip (U = 2 puts 2K loads in flight per lane).
+template <int K, int R, bool NT, int U = 1>
 __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
     Tab T[R][K];
 #pragma unroll
@@ -218,37 +253,26 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
 
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
-    for (UnitIter u(job); u.s < job.nstripes; u.next(job)) {
-        const uint64_t off = static_cast<uint64_t>(u.c) * kChunk;
-        const uint64_t ib = u.s * job.in_sstride + off;
-        const uint64_t ob = u.s * job.out_sstride + off;
-        const bool full = u.c < nfull;
-        const uint32_t nb = full ? kChunk : static_cast<uint32_t>(sz - off);
-        u32x4 x[K];
-        if (full) {
+    UnitIter u(job);
+    while (u.s < job.nstripes) {
+        uint64_t ib[U], ob[U];
+        uint32_t nb[U];
+        bool full[U], live[U];
+        u32x4 x[U][K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + ib);
-        } else {
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = load_tail(job.in[j] + ib, nb);
-        }
-        Sel sel[4][K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            sel[0][j] = selectors(x[j].x);
-            sel[1][j] = selectors(x[j].y);
-            sel[2][j] = selectors(x[j].z);
-            sel[3][j] = selectors(x[j].w);
+        for (int i = 0; i < U; ++i) {
+            live[i] = u.s < job.nstripes;
+            const uint64_t off = static_cast<uint64_t>(u.c) * kChunk;
+            ib[i] = u.s * job.in_sstride + off;
+            ob[i] = u.s * job.out_sstride + off;
+            full[i] = u.c < nfull;
+            nb[i] = full[i] ? kChunk : static_cast<uint32_t>(sz - off);
+            if (live[i]) reg_load<K>(job, x[i], ib[i], full[i], nb[i]);
+            u.next(job);
         }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const u32x4 y{gf_dot<K>(T[r], sel[0]), gf_dot<K>(T[r], sel[1]), gf_dot<K>(T[r], sel[2]),
-                          gf_dot<K>(T[r], sel[3])};
-            if (full)
-                store16_out<NT>(job.out[r] + ob, y);
-            else
-                store_tail(job.out[r] + ob, y, nb);
-        }
+        for (int i = 0; i < U; ++i)
+            if (live[i]) reg_compute_store<K, R, NT>(job, T, x[i], ob[i], full[i], nb[i]);
     }
 }
 
@@ -342,6 +366,7 @@ struct Variant {
     const char* name;
     int max_blocks_per_cu;  // from the occupancy API, cached
     bool kernarg_tables;    // the kernel reads job.tab[] instead of job.coef[]
+    int units_per_lane = 1; // units a lane handles per loop trip (grid sizing)
 };
 
 // Register-table variants: k <= 4, r <= 8.
@@ -430,7 +455,8 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     }
     // One 16-byte unit per lane up to 16x the resident capacity; beyond that a
     // grid-stride loop (the 64 MiB config fits in a single pass).
-    const uint64_t need = (total + kBlock - 1) / kBlock;
+    const uint64_t lanes = (total + v->units_per_lane - 1) / v->units_per_lane;
+    const uint64_t need = (lanes + kBlock - 1) / kBlock;
     const uint64_t cap = static_cast<uint64_t>(g_num_cu) * v->max_blocks_per_cu * g_grid_mult;
     const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
     const uint64_t gstride = static_cast<uint64_t>(grid) * kBlock;

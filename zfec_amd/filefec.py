@@ -1,0 +1,368 @@
+"""filefec -- zfec's share-file format and file encode/decode, on the MI355X engine.
+
+Mirrors /root/reference/zfec/filefec.py: the 1-4 byte bit-packed header
+(`_build_header` :58-118, `_parse_header` :123-181), `encode_to_files`
+(:185-256), `decode_from_files` (:264-316) and the segment callback API
+`encode_file_stringy_easyfec` (:494-522).  Share files are byte-identical to
+the reference's (tests/test_filefec.py checks them against files written by
+the reference itself).
+
+The reference encodes a file segment by segment: each segment is k*4096
+input bytes split easyfec-style into k blocks, and share i is the header
+followed by block i of every segment.  Here a window of W whole segments is
+one GPU call: the window is regrouped block-major ([k][W*4096]; block j of
+the window = block j of every segment, back to back), so ONE encode of k
+blocks of W*4096 bytes yields the m share bodies of the window directly --
+parity rows for i >= k, and the regrouped input rows for i < k.  Decoding is
+the same in reverse: W*4096 bytes of each of k shares are the k blocks of
+one call, and the recovered rows are regrouped segment-major for the output.
+Window buffers are pinned (fec_host_alloc), so the library streams them
+through its overlapped H2D / kernel / D2H pipeline.  Only the final, short
+segment takes the per-segment path.
+"""
+import os
+import struct
+
+import numpy as np
+
+import zfec_amd
+from zfec_amd import capi, easyfec
+
+CHUNKSIZE = 4096
+WINDOW_BYTES = 64 << 20  # input bytes per GPU call (rounded down to whole segments)
+
+
+def pad_size(n, k):
+    """The smallest number that has to be added to n to equal a multiple of k (filefec.py:10-17)."""
+    return k - n % k if n % k else 0
+
+
+def log_ceil(n, b):
+    """The smallest integer k such that b^k >= n (filefec.py:19-31)."""
+    p, k = 1, 0
+    while p < n:
+        p *= b
+        k += 1
+    return k
+
+
+class InsufficientShareFilesError(zfec_amd.Error):
+    def __init__(self, k, kb, *args, **kwargs):
+        zfec_amd.Error.__init__(self, *args, **kwargs)
+        self.k = k
+        self.kb = kb
+
+    def __repr__(self):
+        return ("Insufficient share files -- %d share files are required to recover this file, but only %d were "
+                "given" % (self.k, self.kb))
+
+    def __str__(self):
+        return self.__repr__()
+
+
+class CorruptedShareFilesError(zfec_amd.Error):
+    pass
+
+
+def _build_header(m, k, pad, sh):
+    """Pack (m, k, pad, shnum) into 2-4 bytes (filefec.py:58-118): 8 bits of m-1,
+    then log_ceil(m) bits of k-1, log_ceil(k) bits of pad, log_ceil(m) bits of
+    shnum, left-aligned in the smallest of 2, 3 or 4 bytes."""
+    assert 1 <= m <= 256 and 1 <= k <= m and 0 <= pad < k and 0 <= sh < m
+    fields = [(m - 1, 8), (k - 1, log_ceil(m, 2)), (pad, log_ceil(k, 2)), (sh, log_ceil(m, 2))]
+    val, used = 0, 0
+    for v, bits in fields:
+        val = (val << bits) | v
+        used += bits
+    assert 8 <= used <= 32, used
+    nbytes = 2 if used <= 16 else 3 if used <= 24 else 4
+    val <<= 8 * nbytes - used
+    return struct.pack(">I", val)[4 - nbytes:]
+
+
+def MASK(bits):
+    return (1 << bits) - 1
+
+
+def _truncated(inf):
+    return CorruptedShareFilesError(
+        "Share files were corrupted -- share file %r didn't have a complete metadata header at the front.  "
+        "Perhaps the file was truncated." % (getattr(inf, "name", inf),))
+
+
+def _parse_header(inf):
+    """Read 1-4 header bytes from `inf` and return (m, k, pad, shnum) (filefec.py:123-181)."""
+    ch = inf.read(1)
+    if not ch:
+        raise _truncated(inf)
+    m = ord(ch) + 1
+    kbits = log_ceil(m, 2)
+    b2_bits_left = 8 - kbits
+    kbitmask = MASK(kbits) << b2_bits_left
+    ch = inf.read(1)
+    if not ch:
+        raise _truncated(inf)
+    byte = ord(ch)
+    k = ((byte & kbitmask) >> b2_bits_left) + 1
+    shbits = log_ceil(m, 2)
+    padbits = log_ceil(k, 2)
+    val = byte & ~kbitmask
+    needed_padbits = padbits - b2_bits_left
+    if needed_padbits > 0:
+        ch = inf.read(1)
+        if not ch:
+            raise _truncated(inf)
+        val = (val << 8) | ord(ch)
+        needed_padbits -= 8
+    assert needed_padbits <= 0
+    extrabits = -needed_padbits
+    pad = val >> extrabits
+    val &= MASK(extrabits)
+    needed_shbits = shbits - extrabits
+    if needed_shbits > 0:
+        ch = inf.read(1)
+        if not ch:
+            raise _truncated(inf)
+        val = (val << 8) | ord(ch)
+        needed_shbits -= 8
+    assert needed_shbits <= 0
+    sh = val >> -needed_shbits
+    return (m, k, pad, sh)
+
+
+FORMAT_FORMAT = "%%s.%%0%dd_%%0%dd%%s"
+RE_FORMAT = "%s.[0-9]+_[0-9]+%s"
+
+
+class _PinnedArray(object):
+    """A numpy view over pinned host memory from the engine (fec_host_alloc)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = max(1, nbytes)
+        self.ptr = capi.lib().fec_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError("fec_host_alloc(%d) failed: %s" % (self.nbytes, capi.lib().fec_last_error_message().decode()))
+        import ctypes
+
+        self.array = np.ctypeslib.as_array((ctypes.c_ubyte * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            capi.lib().fec_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+def _readinto_full(inf, view):
+    """Read up to len(view) bytes into `view`; returns the count (short only at EOF)."""
+    got = 0
+    n = len(view)
+    while got < n:
+        if hasattr(inf, "readinto"):
+            r = inf.readinto(view[got:])
+        else:
+            data = inf.read(n - got)
+            r = len(data)
+            view[got:got + r] = data
+        if not r:
+            break
+        got += r
+    return got
+
+
+def encode_to_files(inf, fsize, dirname, prefix, k, m, suffix=".fec", overwrite=False, verbose=False):
+    """Encode inf into m share files named prefix.<shnum>_<m><suffix> in dirname
+    (filefec.py:185-256).  Returns 0, or 1 after removing the partial files if
+    an EnvironmentError occurred."""
+    mlen = len(str(m))
+    fmt = FORMAT_FORMAT % (mlen, mlen)
+    padbytes = pad_size(fsize, k)
+    fns, fs = [], []
+    got_error = False
+    try:
+        for shnum in range(m):
+            hdr = _build_header(m, k, padbytes, shnum)
+            fn = os.path.join(dirname, fmt % (prefix, shnum, m, suffix))
+            if verbose:
+                print("Creating share file %r..." % (fn,))
+            if overwrite:
+                f = open(fn, "wb")
+            else:
+                flags = os.O_WRONLY | os.O_CREAT | os.O_EXCL | (hasattr(os, "O_BINARY") and os.O_BINARY)
+                f = os.fdopen(os.open(fn, flags), "wb")
+            fs.append(f)
+            fns.append(fn)
+            f.write(hdr)
+        _encode_stream(inf, fsize, k, m, fs, verbose)
+    except EnvironmentError as le:
+        print("Cannot complete because of exception: ")
+        print(le)
+        got_error = True
+    finally:
+        for f in fs:
+            f.close()
+        if got_error:
+            print("Cleaning up...")
+            for fn in fns:
+                try:
+                    os.remove(fn)
+                except EnvironmentError:
+                    pass
+            return 1
+    if verbose:
+        print()
+        print("Done!")
+    return 0
+
+
+def _encode_stream(inf, fsize, k, m, fs, verbose):
+    seg = k * CHUNKSIZE
+    wseg = max(1, WINDOW_BYTES // seg)
+    code = capi.Code(k, m)
+    win_in = _PinnedArray(wseg * seg)           # segment-major, as read from the file
+    rows = _PinnedArray(wseg * seg)             # block-major regrouping of win_in
+    par = _PinnedArray((m - k) * wseg * CHUNKSIZE) if m > k else None
+    total = 0
+    try:
+        while True:
+            got = _readinto_full(inf, memoryview(win_in.array)[:wseg * seg])
+            if got == 0:
+                break
+            total += got
+            if total > fsize:
+                raise IOError("Wrong file size -- possibly the size of the file changed during encoding.  "
+                              "Original size: %d, observed size at least: %s" % (fsize, total))
+            nfull = got // seg
+            if nfull:
+                w = nfull * CHUNKSIZE  # bytes per share in this window
+                blk = rows.array[:k * w].reshape(k, nfull, CHUNKSIZE)
+                blk[...] = win_in.array[:nfull * seg].reshape(nfull, k, CHUNKSIZE).transpose(1, 0, 2)
+                if m > k:
+                    code.encode_ptrs([rows.ptr + j * w for j in range(k)],
+                                     [par.ptr + i * w for i in range(m - k)], list(range(k, m)), w,
+                                     flags=capi.FEC_FLAG_LIBRARY_STREAM)
+                for i in range(k):
+                    fs[i].write(memoryview(rows.array)[i * w:(i + 1) * w])
+                for i in range(m - k):
+                    fs[k + i].write(memoryview(par.array)[i * w:(i + 1) * w])
+            rest = got - nfull * seg
+            if rest:  # the final, short segment: easyfec split/pad, as the reference does
+                tail = bytes(win_in.array[nfull * seg:got])
+                for i, b in enumerate(easyfec.Encoder(k, m).encode(tail)):
+                    fs[i].write(b)
+            if verbose:
+                print("%d%% ..." % (100 * total // max(1, fsize)), end=" ")
+            if got < wseg * seg:
+                break
+    finally:
+        for a in (win_in, rows, par):
+            if a is not None:
+                a.free()
+
+
+def decode_from_files(outf, infiles, verbose=False):
+    """Decode from the first k files in infiles, writing the result to outf
+    (filefec.py:264-316)."""
+    assert len(infiles) >= 2
+    infs, shnums = [], []
+    m = k = padlen = None
+    for f in infiles:
+        (nm, nk, npadlen, shnum) = _parse_header(f)
+        if not (m is None or m == nm):
+            raise CorruptedShareFilesError(
+                "Share files were corrupted -- share file %r said that m was %s but another share file previously "
+                "said that m was %s" % (f.name, nm, m))
+        m = nm
+        if not (k is None or k == nk):
+            raise CorruptedShareFilesError(
+                "Share files were corrupted -- share file %r said that k was %s but another share file previously "
+                "said that k was %s" % (f.name, nk, k))
+        if not (k is None or k <= len(infiles)):
+            raise InsufficientShareFilesError(k, len(infiles))
+        k = nk
+        if not (padlen is None or padlen == npadlen):
+            raise CorruptedShareFilesError(
+                "Share files were corrupted -- share file %r said that pad length was %s but another share file "
+                "previously said that pad length was %s" % (f.name, npadlen, padlen))
+        padlen = npadlen
+        infs.append(f)
+        shnums.append(shnum)
+        if len(infs) == k:
+            break
+    if len(infs) < k:
+        raise InsufficientShareFilesError(k, len(infs))
+
+    # slot order: primary i at slot i (zfec/_fecmodule.c:482-493)
+    order = sorted(range(k), key=lambda i: shnums[i])
+    slots = [None] * k
+    rest = [i for i in order if shnums[i] >= k]
+    for i in order:
+        if shnums[i] < k:
+            slots[shnums[i]] = i
+    it = iter(rest)
+    slots = [s if s is not None else next(it) for s in slots]
+    slot_nums = [shnums[i] for i in slots]
+    missing = [j for j in range(k) if slot_nums[j] >= k]
+
+    wseg = max(1, WINDOW_BYTES // (k * CHUNKSIZE))
+    code = capi.Code(k, m)
+    w_max = wseg * CHUNKSIZE
+    ins = _PinnedArray(k * w_max)
+    rec = _PinnedArray(max(1, len(missing)) * w_max)
+    outbuf = _PinnedArray(k * w_max)
+    byteswritten = 0
+    try:
+        while True:
+            lens = [_readinto_full(infs[slots[j]], memoryview(ins.array)[j * w_max:(j + 1) * w_max])
+                    for j in range(k)]
+            if any(n != lens[-1] for n in lens):
+                raise CorruptedShareFilesError(
+                    "Share files were corrupted -- all share files are required to be the same length, but they "
+                    "weren't.")
+            n = lens[-1]
+            if n == 0:
+                break
+            nfull, tail = divmod(n, CHUNKSIZE)
+            if nfull:
+                w = nfull * CHUNKSIZE
+                if missing:
+                    code.decode_ptrs([ins.ptr + j * w_max for j in range(k)],
+                                     [rec.ptr + i * w_max for i in range(len(missing))], slot_nums, w,
+                                     flags=capi.FEC_FLAG_LIBRARY_STREAM)
+                out = outbuf.array[:nfull * k * CHUNKSIZE].reshape(nfull, k, CHUNKSIZE)
+                for j in range(k):
+                    src = ins.array[j * w_max:j * w_max + w] if slot_nums[j] < k else \
+                        rec.array[missing.index(j) * w_max:missing.index(j) * w_max + w]
+                    out[:, j, :] = src.reshape(nfull, CHUNKSIZE)
+                outf.write(memoryview(outbuf.array)[:nfull * k * CHUNKSIZE])
+                byteswritten += nfull * k * CHUNKSIZE
+            if tail:  # the final, short segment of each share
+                blocks = [bytes(ins.array[j * w_max + nfull * CHUNKSIZE:j * w_max + n]) for j in range(k)]
+                data = b"".join(zfec_amd.Decoder(k, m).decode(blocks, slot_nums))
+                outf.write(data)
+                byteswritten += len(data)
+            if verbose:
+                print(str(byteswritten // 10 ** 6) + " MB ...", end=" ")
+            if n < w_max:
+                break
+    finally:
+        for a in (ins, rec, outbuf):
+            a.free()
+    if padlen:
+        outf.truncate(byteswritten - padlen)
+    if verbose:
+        print()
+        print("Done!")
+
+
+def encode_file_stringy_easyfec(inf, cb, k, m, chunksize=4096):
+    """Segment callback API (filefec.py:494-522): read chunksize*k bytes at a
+    time, encode with easyfec, call cb(blocks, length)."""
+    enc = easyfec.Encoder(k, m)
+    readsize = k * chunksize
+    indata = inf.read(readsize)
+    while indata:
+        cb(enc.encode(indata), len(indata))
+        indata = inf.read(readsize)
