@@ -15,6 +15,7 @@
 #include <cstring>
 #include <algorithm>
 #include <vector>
+#include <array>
 
 using namespace zfec_hip;
 
@@ -111,48 +112,72 @@ int main(int argc, char** argv) {
             CK(hipFree(xout));
         }
     }
-    if (getenv("MB_AB")) {  // interleaved A/B of store policy: 7 rounds, median (guide §5.4 rule 24)
+    if (getenv("MB_AB")) {  // interleaved A/B of general-kernel variants: 7 rounds, median (guide §5.4 rule 24)
         struct V {
             const char* name;
             KernelFn fn;
-            int k, r;
-            bool ktab;
+            bool ktab, lds;
+            int chunk;
         } vs[] = {
-            {"reg<3,7> nt", matapply_reg<3, 7, true, 1>, 3, 7, true},
-            {"reg<3,7> plain", matapply_reg<3, 7, false, 1>, 3, 7, true},
-            {"reg<3,3> nt", matapply_reg<3, 3, true, 1>, 3, 3, true},
-            {"reg<3,3> plain", matapply_reg<3, 3, false, 1>, 3, 3, true},
-            {"gen<ktab> 10x6 nt", matapply_gen<false, true, true>, 10, 6, true},
-            {"gen<ktab> 10x6 plain", matapply_gen<false, false, true>, 10, 6, true},
-            {"gen 20x40 nt", matapply_gen<false, true, false>, 20, 40, false},
-            {"gen 20x40 plain", matapply_gen<false, false, false>, 20, 40, false},
+            {"lds<8,4,4>", matapply_lds<false, true, 8, 4, 4>, false, true, 16},
+            {"lds<8,2,4>", matapply_lds<false, true, 8, 2, 4>, false, true, 8},
+            {"lds<16,2,4>", matapply_lds<false, true, 16, 2, 4>, false, true, 8},
+            {"lds<8,2,8>", matapply_lds<false, true, 8, 2, 8>, false, true, 8},
+            {"lds<16,2,2>", matapply_lds<false, true, 16, 2, 2>, false, true, 8},
+            {"lds<4,4,8>", matapply_lds<false, true, 4, 4, 8>, false, true, 16},
+            {"lds<8,4,8>", matapply_lds<false, true, 8, 4, 8>, false, true, 16},
         };
-        const int nv = sizeof(vs) / sizeof(vs[0]);
-        std::vector<std::vector<float>> t(nv);
-        std::vector<uint8_t*> ins(nv), outs(nv);
-        std::vector<size_t> bszs(nv);
-        for (int i = 0; i < nv; ++i) {
-            bszs[i] = (S / vs[i].k + 255) / 256 * 256;
-            CK(hipMalloc(&ins[i], vs[i].k * bszs[i]));
-            CK(hipMalloc(&outs[i], vs[i].r * bszs[i]));
-            CK(hipMemset(ins[i], 0x5a, vs[i].k * bszs[i]));
+        const int shapes_all[][2] = {{10, 6}, {10, 4}, {5, 8}, {20, 40}, {20, 20}, {16, 16}, {32, 32}, {8, 8}, {3, 17}, {12, 12}};
+        std::vector<std::array<int, 2>> shapes;
+        if (const char* e = getenv("MB_SHAPE")) {  // "k,r": one shape only (for counter runs)
+            int a = 0, b = 0;
+            sscanf(e, "%d,%d", &a, &b);
+            shapes.push_back({a, b});
+        } else {
+            for (auto& sh : shapes_all) shapes.push_back({sh[0], sh[1]});
         }
-        for (int round = 0; round < 7; ++round)
-            for (int i = 0; i < nv; ++i) {
-                Variant* slot = vs[i].k <= kRegK && vs[i].r <= kRegR ? &g_reg[vs[i].k][vs[i].r]
-                                : (vs[i].ktab ? &g_gen_tab : &g_gen);
-                const Variant saved = *slot;
-                *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1};
-                g_grid_mult = 16;
-                MatJob j = make_job(ins[i], outs[i], vs[i].k, vs[i].r, bszs[i], bszs[i]);
-                t[i].push_back(time_ms([&] { MatJob jj = j; CK(launch_matapply(jj, 0)); }, 10));
-                *slot = saved;
+        const char* only = getenv("MB_VARIANT");  // one variant name only
+        const int nv = sizeof(vs) / sizeof(vs[0]);
+        for (auto& sh : shapes) {
+            const int k = sh[0], r = sh[1];
+            const size_t bsz = (S / k + 255) / 256 * 256;
+            uint8_t *xin, *xout;
+            CK(hipMalloc(&xin, k * bsz));
+            CK(hipMalloc(&xout, r * bsz));
+            CK(hipMemset(xin, 0x5a, k * bsz));
+            std::vector<std::vector<float>> t(nv);
+            std::vector<uint8_t> want(r * bsz), got(r * bsz);
+            {
+                MatJob j = make_job(xin, xout, k, r, bsz, bsz);
+                CK(launch_matapply(j, 0));
+                CK(hipMemcpy(want.data(), xout, r * bsz, hipMemcpyDeviceToHost));
             }
-        for (int i = 0; i < nv; ++i) {
-            std::sort(t[i].begin(), t[i].end());
-            const double by = double(vs[i].k + vs[i].r) * bszs[i];
-            printf("AB %-22s median %8.4f ms (min %8.4f)  hbm %7.1f GB/s\n", vs[i].name, t[i][3], t[i][0],
-                   by / (t[i][3] * 1e-3) / 1e9);
+            for (int round = 0; round < 7; ++round)
+                for (int i = 0; i < nv; ++i) {
+                    if (vs[i].ktab && k * r > kMaxKernargTables) continue;
+                    if (only && strcmp(only, vs[i].name)) continue;
+                    Variant* slot = k <= kRegK && r <= kRegR ? &g_reg[k][r] : (r <= 8 ? &g_lds_narrow : &g_lds_wide);
+                    const Variant saved = *slot;
+                    *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1, vs[i].lds, vs[i].chunk};
+                    g_grid_mult = 16;
+                    MatJob j = make_job(xin, xout, k, r, bsz, bsz);
+                    if (round == 0) CK(hipMemset(xout, 0, r * bsz));
+                    t[i].push_back(time_ms([&] { MatJob jj = j; CK(launch_matapply(jj, 0)); }, 10));
+                    *slot = saved;
+                    if (round == 0) {
+                        CK(hipMemcpy(got.data(), xout, r * bsz, hipMemcpyDeviceToHost));
+                        if (memcmp(got.data(), want.data(), r * bsz)) printf("MISMATCH k=%d r=%d %s\n", k, r, vs[i].name);
+                    }
+                }
+            for (int i = 0; i < nv; ++i) {
+                if (t[i].empty()) continue;
+                std::sort(t[i].begin(), t[i].end());
+                const double by = double(k + r) * bsz;
+                printf("AB k=%2d r=%2d %-10s median %8.4f ms  hbm %7.1f GB/s  input %7.1f GB/s\n", k, r, vs[i].name,
+                       t[i][3], by / (t[i][3] * 1e-3) / 1e9, double(k) * bsz / (t[i][3] * 1e-3) / 1e9);
+            }
+            CK(hipFree(xin));
+            CK(hipFree(xout));
         }
         return 0;
     }

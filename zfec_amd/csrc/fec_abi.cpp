@@ -199,7 +199,7 @@ int apply_matrix(const uint8_t* coef /* r x k */, unsigned k, unsigned r, const 
                  uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
                  hipStream_t stream) {
     if (r == 0 || sz == 0 || nstripes == 0) return FEC_OK;
-    const size_t cps = (sz + kChunk - 1) / kChunk;
+    const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
     const size_t max_units = size_t(1) << 31;
     const size_t stripes_per_launch = std::max<size_t>(1, max_units / cps);
     if (cps > max_units) return set_status(FEC_EINVAL, "block size %zu too large for one launch", sz);

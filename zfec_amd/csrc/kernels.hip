@@ -5,30 +5,31 @@
 // (fec.c:487-505) and fec_decode (fec.c:527-557).  Here one kernel reads each
 // input chunk from HBM once and produces every requested output from it:
 //
-//   * each lane owns a 16-byte column slice of every block (one
-//     global_load_dwordx4 per input block, 1 KiB coalesced per wave);
+//   * each lane owns a 16-byte (or 8-byte) column slice of every block, so a
+//     wave's loads and stores are 1 KiB (512 B) contiguous;
 //   * multiplication by a constant c is GF(2)-linear, so
 //       c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]
 //     with three 8/8/4-entry byte tables; v_perm_b32 looks up four bytes at
 //     once in an 8-byte table held in a register pair;
 //   * partial products are merged by v_bitop3_b32 (gfx950's 3-input logic
-//     op; truth table 0x96 = XOR3);
-//   * the tables of all 256 byte values are a compile-time bank in constant
-//     memory (8 KiB); a wave-uniform coefficient becomes two scalar loads, so
-//     tables live in SGPRs and never cost LDS bandwidth or VGPRs.
+//     op; truth table 0x96 = XOR3).
 //
 // Two shapes of kernel:
 //   matapply_reg<K, R>  compile-time k <= 4 and r <= 8 (encode K=3/M=10 is
-//                       <3,7>, its decode <3,3>): every table is loaded once
-//                       per lane, the per-chunk body is straight-line code.
-//   matapply_gen        any k <= 32, r <= 48: rows in register tiles of RT,
-//                       inputs streamed in groups of G with loads one group
-//                       ahead, tables fetched per use by scalar loads.
+//                       <3,7>, its decode <3,3>): all K*R tables arrive in the
+//                       kernel arguments and stay in registers; the per-chunk
+//                       body is straight-line code.
+//   matapply_lds        any k <= 32, r <= 48 (longer codes are split by the
+//                       caller): each workgroup expands its coefficients into
+//                       LDS tables from a compile-time bank of all 256 values;
+//                       rows in register tiles, inputs in prefetched groups.
 //
-// Cost per input byte: 3 v_perm + ~1.5 v_bitop3 per output row / 4 bytes,
-// i.e. ~9 VALU ops at K=3/M=10; the HBM roofline needs ~15 T ops/s of the
-// chip's ~78 T, so the K=3/M=10 kernels are memory-bound (measured: they move
-// bytes as fast as a copy kernel with the same load/store pattern).
+// Measured issue rates on gfx950 (tools/mb_valu.hip): v_perm_b32 and
+// v_bitop3_b32 (VOP3) sustain ~37 T lane-ops/s chip-wide, plain VOP2 ops
+// ~60 T.  A coefficient costs 3 v_perm + 1.5 v_bitop3 per 4 bytes, so K=3/M=10
+// (~9 VOP3 per input byte, ~22 T ops/s at the HBM roofline) is memory-bound,
+// while wide codes are bound by VALU issue (K=20/M=60: 45 VOP3 per input
+// byte, <= ~0.8 TB/s of input).
 #include "kernels.hpp"
 
 #include <hip/hip_runtime.h>
@@ -99,21 +100,10 @@ struct Tab {
     uint32_t w0, w1, w2, w3, w4;
 };
 
-__device__ __forceinline__ Tab table_of(uint32_t c) {
-    const uint32_t* t = &g_bank.w[c * 8];
-    return Tab{t[0], t[1], t[2], t[3], t[4]};
-}
-
 // Table of coefficient i (row-major r x k) from the kernel arguments.
 __device__ __forceinline__ Tab karg_table(const MatJob& job, uint32_t i) {
     const uint32_t* t = &job.tab[i * 5];
     return Tab{t[0], t[1], t[2], t[3], t[4]};
-}
-
-// Byte i of the kernarg coefficient array, fetched as a scalar dword.
-__device__ __forceinline__ uint32_t coef_at(const MatJob& job, uint32_t i) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(job.coef)[i >> 2];
-    return (w >> (8 * (i & 3))) & 0xFFu;
 }
 
 // ---- arithmetic ---------------------------------------------------------------
@@ -124,14 +114,6 @@ struct Sel {
 
 __device__ __forceinline__ Sel selectors(uint32_t x) {
     return Sel{x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
-}
-
-// acc ^ c*x for four bytes: 3 v_perm_b32 + 2 v_bitop3_b32.
-__device__ __forceinline__ uint32_t gf_mac(uint32_t acc, const Tab& t, Sel s) {
-    const uint32_t a = perm(t.w1, t.w0, s.s0);
-    const uint32_t b = perm(t.w3, t.w2, s.s1);
-    const uint32_t d = perm(t.w4, t.w4, s.s2);
-    return xor3(xor3(acc, a, b), d, 0u);
 }
 
 // sum_j c_j*x_j for four bytes of one output row: the 3K partial products are
@@ -277,82 +259,217 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
 }
 
 // ---------------------------------------------------------------------------
-// matapply_gen: runtime k (<= kMaxIn) and r (<= kMaxOut).  Rows are produced
-// in register tiles of RT; inside a tile the inputs stream through in groups
-// of G blocks whose loads are issued one group ahead.  Each (row, input)
-// table arrives by scalar loads: from the kernel arguments when k*r <=
-// kMaxKernargTables (KTAB), else coefficient byte -> bank.  ACC: XOR into the
-// existing output (continuation launches for k > kMaxIn).
+// matapply_lds<ACC, NT, RT>: runtime k and r like matapply_gen, but each
+// workgroup first expands its k*r coefficients into LDS tables (32 bytes per
+// coefficient).  In the loop a table is two broadcast LDS reads off one base
+// address straight into VGPRs, so v_perm_b32 gets all-VGPR operands (gfx9's
+// one-SGPR-per-VALU-op limit forces a v_mov per table word pair on the
+// scalar path) and no scalar load -> dependent load chain sits in the loop.
+// Inputs go in pairs so six partial products share three XOR3s, and rows
+// past r in the last tile are skipped by a wave-uniform branch.
 // ---------------------------------------------------------------------------
-constexpr int RT = 8;
-constexpr int G = 4;
+struct LdsTab {
+    u32x4 w03;  // c*{0..7} and c*{0,8,..,56}
+    u32x4 w4;   // c*{0,64,128,192}, 3 pad words (keeps both reads on one base address)
+};
 
-__device__ __forceinline__ void load_group(u32x4 (&x)[G], const MatJob& job, uint32_t g, uint32_t k, uint64_t ib,
-                                           bool full, uint32_t nb) {
+__device__ __forceinline__ void lds_tables_build(const MatJob& job, LdsTab* t) {
+    const uint32_t n = job.k * job.r;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        // entry (input j, row) at j * r + row: a tile's rows for one input are adjacent
+        const uint32_t j = i / job.r, row = i - j * job.r;
+        const uint32_t c = job.coef[row * job.k + j];
+        const uint32_t* b = &g_bank.w[c * 8];
+        t[i].w03 = u32x4{b[0], b[1], b[2], b[3]};
+        t[i].w4 = u32x4{b[4], 0u, 0u, 0u};
+    }
+    __syncthreads();
+}
+
+// acc ^ c0*x0 ^ c1*x1 for four bytes: 6 v_perm_b32 + 3 v_bitop3_b32.
+__device__ __forceinline__ uint32_t gf_mac2(uint32_t acc, const u32x4& t0, uint32_t u0, Sel s0, const u32x4& t1,
+                                            uint32_t u1, Sel s1) {
+    const uint32_t a0 = perm(t0.y, t0.x, s0.s0), b0 = perm(t0.w, t0.z, s0.s1), d0 = perm(u0, u0, s0.s2);
+    const uint32_t a1 = perm(t1.y, t1.x, s1.s0), b1 = perm(t1.w, t1.z, s1.s1), d1 = perm(u1, u1, s1.s2);
+    return xor3(xor3(xor3(acc, a0, b0), d0, a1), b1, d1);
+}
+
+__device__ __forceinline__ uint32_t gf_mac_v(uint32_t acc, const u32x4& t, uint32_t t4, Sel s) {
+    const uint32_t a = perm(t.y, t.x, s.s0);
+    const uint32_t b = perm(t.w, t.z, s.s1);
+    const uint32_t d = perm(t4, t4, s.s2);
+    return xor3(xor3(acc, a, b), d, 0u);
+}
+
+// D dwords per lane per block (chunk = 4*D bytes): D = 4 is one dwordx4 per
+// block, D = 2 halves the accumulator / selector / input registers so more
+// waves fit per SIMD.
+template <int D>
+struct Words {
+    uint32_t w[D];
+};
+
+template <int D>
+__device__ __forceinline__ Words<D> load_words(const uint8_t* p, bool full, uint32_t nb) {
+    Words<D> x;
+    if (full) {
+        __builtin_memcpy(x.w, p, 4 * D);
+    } else {
+        const u32x4 t = load_tail(p, nb);
+        const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-    for (int jj = 0; jj < G; ++jj) {
-        const uint32_t j = g + jj;
-        if (j < k)
-            x[jj] = full ? load16(job.in[j] + ib) : load_tail(job.in[j] + ib, nb);
-        else
-            x[jj] = u32x4{0u, 0u, 0u, 0u};
+        for (int v = 0; v < D; ++v) x.w[v] = tw[v];
+    }
+    return x;
+}
+
+template <int D, bool NT>
+__device__ __forceinline__ void store_words(uint8_t* p, const Words<D>& y, bool full, uint32_t nb) {
+    if (full) {
+        if constexpr (D == 4) {
+            store16_out<NT>(p, u32x4{y.w[0], y.w[1], y.w[2], y.w[3]});
+        } else if constexpr (D == 2) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v{y.w[0], y.w[1]};
+            if constexpr (NT)
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+            else
+                __builtin_memcpy(p, &v, 8);
+        } else {
+            __builtin_memcpy(p, y.w, 4 * D);
+        }
+    } else {
+        u32x4 t{0u, 0u, 0u, 0u};
+        t.x = y.w[0];
+        if constexpr (D > 1) t.y = y.w[1];
+        if constexpr (D > 2) t.z = y.w[2];
+        if constexpr (D > 3) t.w = y.w[3];
+        store_tail(p, t, nb);
     }
 }
 
-template <bool ACC, bool NT, bool KTAB>
-__global__ __launch_bounds__(kBlock) void matapply_gen(const MatJob job) {
+// One step of the flattened (unit, row tile, input group) walk.
+struct Step {
+    UnitIter u;
+    uint32_t rb, g;
+};
+
+template <bool ACC, bool NT, int RT_, int D, int GG>
+__global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
+    constexpr uint32_t CH = 4 * D;
+    extern __shared__ LdsTab lds_tab[];
     const uint32_t k = job.k;
     const uint32_t r = job.r;
+    lds_tables_build(job, lds_tab);
     const uint64_t sz = job.sz;
-    const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
-    for (UnitIter u(job); u.s < job.nstripes; u.next(job)) {
-        const uint64_t off = static_cast<uint64_t>(u.c) * kChunk;
-        const uint64_t ib = u.s * job.in_sstride + off;
-        const uint64_t ob = u.s * job.out_sstride + off;
-        const bool full = u.c < nfull;
-        const uint32_t nb = full ? kChunk : static_cast<uint32_t>(sz - off);
-        for (uint32_t rb = 0; rb < r; rb += RT) {
-            uint32_t a[RT][4];
+    const uint32_t nfull = static_cast<uint32_t>(sz / CH);
+    // The walk visits, for each of this lane's units in grid-stride order, each
+    // row tile and, inside it, each group of GG inputs.  The loads of the next
+    // step's group (possibly the next tile's first group, or the next unit's)
+    // are issued before the current group is computed, so a wave never starts
+    // a group waiting on HBM.  (rb, g) are wave-uniform; units differ per lane.
+    auto load_step = [&](const Step& st, Words<D> (&x)[GG]) {
+        const uint64_t off = static_cast<uint64_t>(st.u.c) * CH;
+        const uint64_t ib = st.u.s * job.in_sstride + off;
+        const bool full = st.u.c < nfull;
+        const uint32_t nb = full ? CH : static_cast<uint32_t>(sz - off);
 #pragma unroll
-            for (int rr = 0; rr < RT; ++rr) a[rr][0] = a[rr][1] = a[rr][2] = a[rr][3] = 0u;
-            u32x4 xa[G];
-            load_group(xa, job, 0, k, ib, full, nb);
-            for (uint32_t g = 0; g < k; g += G) {
-                u32x4 xb[G];
-                load_group(xb, job, g + G, k, ib, full, nb);
+        for (int jj = 0; jj < GG; ++jj)
+            if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, full, nb);
+    };
+    Step cur{UnitIter(job), 0u, 0u};
+    const bool live0 = cur.u.s < job.nstripes;
+    Words<D> xa[GG];
+    if (live0) load_step(cur, xa);
+    uint32_t a[RT_][D];
 #pragma unroll
-                for (int jj = 0; jj < G; ++jj) {
-                    const uint32_t j = g + jj;
-                    if (j >= k) break;
-                    const Sel s[4] = {selectors(xa[jj].x), selectors(xa[jj].y), selectors(xa[jj].z),
-                                      selectors(xa[jj].w)};
+    for (int rr = 0; rr < RT_; ++rr)
 #pragma unroll
-                    for (int rr = 0; rr < RT; ++rr) {
-                        const uint32_t row = rb + rr;
-                        Tab t;
-                        if constexpr (KTAB)
-                            t = row < r ? karg_table(job, row * k + j) : table_of(0u);
-                        else
-                            t = table_of(row < r ? coef_at(job, row * k + j) : 0u);
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) a[rr][v] = gf_mac(a[rr][v], t, s[v]);
-                    }
-                }
-#pragma unroll
-                for (int jj = 0; jj < G; ++jj) xa[jj] = xb[jj];
-            }
-#pragma unroll
-            for (int rr = 0; rr < RT; ++rr) {
-                if (rb + rr >= r) break;
-                uint8_t* op = job.out[rb + rr] + ob;
-                u32x4 y{a[rr][0], a[rr][1], a[rr][2], a[rr][3]};
-                if constexpr (ACC) y ^= full ? load16(op) : load_tail(op, nb);
-                if (full)
-                    store16_out<NT>(op, y);
-                else
-                    store_tail(op, y, nb);
+        for (int v = 0; v < D; ++v) a[rr][v] = 0u;
+    // Every lane walks the same (rb, g) sequence; a lane whose units ran out
+    // keeps stepping (without memory traffic) until the whole wave is done.
+    bool live = live0;
+    while (__any(live)) {
+        Step nxt = cur;
+        nxt.g += GG;
+        const bool tile_end = nxt.g >= k;
+        if (tile_end) {
+            nxt.g = 0;
+            nxt.rb += RT_;
+            if (nxt.rb >= r) {
+                nxt.rb = 0;
+                nxt.u.next(job);
             }
         }
+        const bool nlive = nxt.u.s < job.nstripes;
+        Words<D> xb[GG];
+        if (nlive) load_step(nxt, xb);
+        if (live) {
+#pragma unroll
+            for (int jj = 0; jj < GG; jj += 2) {
+                const uint32_t j = cur.g + jj;
+                if (j >= k) break;
+                Sel s0[D];
+#pragma unroll
+                for (int v = 0; v < D; ++v) s0[v] = selectors(xa[jj].w[v]);
+                const LdsTab* t0 = lds_tab + j * r + cur.rb;
+                if (j + 1 < k) {  // two inputs: their six partial products share three XOR3s
+                    Sel s1[D];
+#pragma unroll
+                    for (int v = 0; v < D; ++v) s1[v] = selectors(xa[jj + 1].w[v]);
+                    const LdsTab* t1 = t0 + r;
+#pragma unroll
+                    for (int rr = 0; rr < RT_; ++rr) {
+                        if (cur.rb + rr < r) {  // wave-uniform
+                            const u32x4 p = t0[rr].w03, q = t1[rr].w03;
+                            const uint32_t pu = t0[rr].w4.x, qu = t1[rr].w4.x;
+#pragma unroll
+                            for (int v = 0; v < D; ++v) a[rr][v] = gf_mac2(a[rr][v], p, pu, s0[v], q, qu, s1[v]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int rr = 0; rr < RT_; ++rr) {
+                        if (cur.rb + rr < r) {
+                            const u32x4 p = t0[rr].w03;
+                            const uint32_t pu = t0[rr].w4.x;
+#pragma unroll
+                            for (int v = 0; v < D; ++v) a[rr][v] = gf_mac_v(a[rr][v], p, pu, s0[v]);
+                        }
+                    }
+                }
+            }
+            if (tile_end) {
+                const uint64_t off = static_cast<uint64_t>(cur.u.c) * CH;
+                const uint64_t ob = cur.u.s * job.out_sstride + off;
+                const bool full = cur.u.c < nfull;
+                const uint32_t nb = full ? CH : static_cast<uint32_t>(sz - off);
+#pragma unroll
+                for (int rr = 0; rr < RT_; ++rr) {
+                    if (cur.rb + rr >= r) continue;
+                    uint8_t* op = job.out[cur.rb + rr] + ob;
+                    Words<D> y;
+#pragma unroll
+                    for (int v = 0; v < D; ++v) y.w[v] = a[rr][v];
+                    if constexpr (ACC) {
+                        const Words<D> o = load_words<D>(op, full, nb);
+#pragma unroll
+                        for (int v = 0; v < D; ++v) y.w[v] ^= o.w[v];
+                    }
+                    store_words<D, NT>(op, y, full, nb);
+                }
+            }
+        }
+        if (tile_end) {
+#pragma unroll
+            for (int rr = 0; rr < RT_; ++rr)
+#pragma unroll
+                for (int v = 0; v < D; ++v) a[rr][v] = 0u;
+        }
+#pragma unroll
+        for (int jj = 0; jj < GG; ++jj) xa[jj] = xb[jj];
+        cur = nxt;
+        live = nlive;
     }
 }
 
@@ -367,6 +484,8 @@ struct Variant {
     int max_blocks_per_cu;  // from the occupancy API, cached
     bool kernarg_tables;    // the kernel reads job.tab[] instead of job.coef[]
     int units_per_lane = 1; // units a lane handles per loop trip (grid sizing)
+    bool lds_tables = false; // dynamic LDS of 32 bytes per coefficient
+    int chunk = kChunk;      // bytes per unit (a lane's slice of one block)
 };
 
 // Register-table variants: k <= 4, r <= 8.
@@ -382,7 +501,7 @@ const char* const kRegNames[kRegK + 1][kRegR + 1] = {
     {"", "matapply_reg<4,1>", "matapply_reg<4,2>", "matapply_reg<4,3>", "matapply_reg<4,4>", "matapply_reg<4,5>",
      "matapply_reg<4,6>", "matapply_reg<4,7>", "matapply_reg<4,8>"}};
 Variant g_reg[kRegK + 1][kRegR + 1];
-Variant g_gen, g_gen_acc, g_gen_tab;
+Variant g_lds_fewin, g_lds_narrow, g_lds_wide, g_lds_acc;
 std::once_flag g_dispatch_once;
 int g_num_cu = 0;
 int g_grid_mult = 16;  // grid cap = CUs x resident blocks per CU x g_grid_mult
@@ -409,9 +528,13 @@ void init_dispatch() {
     fill_reg_row<2>();
     fill_reg_row<3>();
     fill_reg_row<4>();
-    g_gen = Variant{matapply_gen<false, true, false>, "matapply_gen", 0, false};
-    g_gen_tab = Variant{matapply_gen<false, true, true>, "matapply_gen<ktab>", 0, true};
-    g_gen_acc = Variant{matapply_gen<true, false, false>, "matapply_gen<acc>", 0, false};
+    // measured (tools/mb_encode.exe MB_AB): k <= 4 (memory-bound) takes 16
+    // bytes per lane in 8-row tiles; otherwise 8 bytes per lane, 8-row tiles
+    // with 4-input groups for r <= 8, 16-row tiles with 2-input groups above
+    g_lds_fewin = Variant{matapply_lds<false, true, 8, 4, 4>, "matapply_lds<8,4,4>", 0, false, 1, true, 16};
+    g_lds_narrow = Variant{matapply_lds<false, true, 8, 2, 4>, "matapply_lds<8,2,4>", 0, false, 1, true, 8};
+    g_lds_wide = Variant{matapply_lds<false, true, 16, 2, 2>, "matapply_lds<16,2,2>", 0, false, 1, true, 8};
+    g_lds_acc = Variant{matapply_lds<true, false, 16, 2, 2>, "matapply_lds<16,2,2,acc>", 0, false, 1, true, 8};
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) {
         hipDeviceProp_t prop;
@@ -423,10 +546,10 @@ void init_dispatch() {
 
 Variant* pick(uint32_t k, uint32_t r, bool acc) {
     std::call_once(g_dispatch_once, init_dispatch);
-    if (acc) return &g_gen_acc;
+    if (acc) return &g_lds_acc;
     if (k >= 1 && k <= static_cast<uint32_t>(kRegK) && r >= 1 && r <= static_cast<uint32_t>(kRegR)) return &g_reg[k][r];
-    if (k * r <= static_cast<uint32_t>(kMaxKernargTables)) return &g_gen_tab;
-    return &g_gen;
+    if (k <= 4) return &g_lds_fewin;
+    return r <= 8 ? &g_lds_narrow : &g_lds_wide;
 }
 
 }  // namespace
@@ -439,15 +562,17 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     if (job.k == 0 || job.k > static_cast<uint32_t>(kMaxIn) || job.r == 0 || job.r > static_cast<uint32_t>(kMaxOut) ||
         job.r * job.k > static_cast<uint32_t>(kMaxCoef) || job.nstripes == 0 || job.sz == 0)
         return hipErrorInvalidValue;
-    const uint64_t cps = (job.sz + kChunk - 1) / kChunk;
+    Variant* v = pick(job.k, job.r, job.accumulate != 0);
+    const uint64_t cps = (job.sz + v->chunk - 1) / v->chunk;
     const uint64_t total = cps * job.nstripes;
     if (total >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits larger jobs
     job.cps = static_cast<uint32_t>(cps);
 
-    Variant* v = pick(job.k, job.r, job.accumulate != 0);
+    const size_t lds = v->lds_tables ? size_t(job.k) * job.r * 32 : 0;
     if (v->max_blocks_per_cu == 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v->fn), kBlock, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v->fn), kBlock,
+                                                         v->lds_tables ? kMaxCoef * 32 : 0) !=
                 hipSuccess ||
             nb <= 0)
             nb = 1;
@@ -470,7 +595,7 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
             for (int q = 0; q < 5; ++q) job.tab[i * 5 + q] = kHostBank.w[c[i] * 8 + q];
         job.tables = 1;
     }
-    hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), 0, stream, job);
+    hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, job);
     return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ constexpr int kMaxIn = 32;     // input blocks per launch (larger k: XOR-accumul
 constexpr int kMaxOut = 48;    // output blocks per launch
 constexpr int kMaxCoef = 1536; // r*k coefficients per launch
 constexpr int kChunk = 16;     // bytes per lane per block per step (one dwordx4)
+constexpr int kMinChunk = 4;   // smallest unit any kernel variant uses (launch splitting)
 constexpr int kBlock = 256;    // threads per workgroup
 
 // Kernel argument block (passed by value; ~2.2 KiB, well inside the kernarg limit).
