@@ -185,6 +185,26 @@ struct UnitIter {
     }
 };
 
+// Byte span of chunk c of a block of sz bytes.  Chunks are CH bytes; the last
+// one, when sz is not a multiple of CH, is shifted back to end at sz and so
+// overlaps its neighbour: both lanes compute and store identical bytes there,
+// and every lane stays on the full-width load/store path.  Blocks shorter
+// than CH, and accumulating launches (XOR into the output is not idempotent),
+// take the byte-wise tail instead.
+struct Span {
+    uint64_t off;
+    bool full;
+    uint32_t nb;
+};
+
+template <uint32_t CH, bool OVERLAP>
+__device__ __forceinline__ Span chunk_span(uint32_t c, uint64_t sz, uint32_t nfull) {
+    const uint64_t off = static_cast<uint64_t>(c) * CH;
+    if (c < nfull) return Span{off, true, CH};
+    if (OVERLAP && sz >= CH) return Span{sz - CH, true, CH};
+    return Span{off, false, static_cast<uint32_t>(sz - off)};
+}
+
 // ---------------------------------------------------------------------------
 // matapply_reg<K, R>: compile-time k and r.  All K*R tables come with the
 // kernel arguments (prefetched scalar loads); the compiler keeps the high
@@ -244,11 +264,11 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             live[i] = u.s < job.nstripes;
-            const uint64_t off = static_cast<uint64_t>(u.c) * kChunk;
-            ib[i] = u.s * job.in_sstride + off;
-            ob[i] = u.s * job.out_sstride + off;
-            full[i] = u.c < nfull;
-            nb[i] = full[i] ? kChunk : static_cast<uint32_t>(sz - off);
+            const Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
+            ib[i] = u.s * job.in_sstride + sp.off;
+            ob[i] = u.s * job.out_sstride + sp.off;
+            full[i] = sp.full;
+            nb[i] = sp.nb;
             if (live[i]) reg_load<K>(job, x[i], ib[i], full[i], nb[i]);
             u.next(job);
         }
@@ -369,13 +389,11 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
     // are issued before the current group is computed, so a wave never starts
     // a group waiting on HBM.  (rb, g) are wave-uniform; units differ per lane.
     auto load_step = [&](const Step& st, Words<D> (&x)[GG]) {
-        const uint64_t off = static_cast<uint64_t>(st.u.c) * CH;
-        const uint64_t ib = st.u.s * job.in_sstride + off;
-        const bool full = st.u.c < nfull;
-        const uint32_t nb = full ? CH : static_cast<uint32_t>(sz - off);
+        const Span sp = chunk_span<CH, !ACC>(st.u.c, sz, nfull);
+        const uint64_t ib = st.u.s * job.in_sstride + sp.off;
 #pragma unroll
         for (int jj = 0; jj < GG; ++jj)
-            if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, full, nb);
+            if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
     };
     Step cur{UnitIter(job), 0u, 0u};
     const bool live0 = cur.u.s < job.nstripes;
@@ -440,10 +458,10 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
                 }
             }
             if (tile_end) {
-                const uint64_t off = static_cast<uint64_t>(cur.u.c) * CH;
-                const uint64_t ob = cur.u.s * job.out_sstride + off;
-                const bool full = cur.u.c < nfull;
-                const uint32_t nb = full ? CH : static_cast<uint32_t>(sz - off);
+                const Span sp = chunk_span<CH, !ACC>(cur.u.c, sz, nfull);
+                const uint64_t ob = cur.u.s * job.out_sstride + sp.off;
+                const bool full = sp.full;
+                const uint32_t nb = sp.nb;
 #pragma unroll
                 for (int rr = 0; rr < RT_; ++rr) {
                     if (cur.rb + rr >= r) continue;
