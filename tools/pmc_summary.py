@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile_round.sh run into profiles/.
 
-Reads gpurun_out/<tag>/{ktrace,fetch,write}/*.csv (rocprofv3 --output-format
-csv) and writes:
-  profiles/<tag>_kernel_stats.csv   rocprofv3's own --stats summary (copied)
-  profiles/<tag>_pmc.json           per (kernel, grid) dispatch group: calls,
-                                    mean duration, FETCH/WRITE per launch
-  profiles/pmc_summary.json         the bench's dominant kernels (read by bench.py)
+Reads gpurun_out/<tag>/<workload>/{ktrace,fetch,write}/*.csv (rocprofv3
+--output-format csv) and writes:
+  profiles/<tag>_<workload>_kernel_stats.csv  rocprofv3's own --stats summary (copied)
+  profiles/<tag>_pmc.json       per workload and role (encode/decode): launches,
+                                mean duration, FETCH/WRITE per launch
+  profiles/pmc_summary.json     {"encode_<workload>": ..., "decode_<workload>": ...}
+                                (read by bench.py for roofline.traffic)
+
+Roles come from dispatch order, which bench.py fixes (run_workload): one
+encode, then (encode, decode) pairs for warmup + 3 + steps, then 20 encodes
+and 20 decodes back to back.  Encode and decode of one workload can be the
+same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes 6), so
+names alone do not tell them apart.
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE (KiB) reads exactly half
 of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is
@@ -17,9 +24,9 @@ import json
 import os
 import shutil
 import sys
-from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B2B = 20
 
 
 def short(name):
@@ -32,45 +39,71 @@ def load(path):
         return list(csv.DictReader(f))
 
 
-def main(tag):
-    src = os.path.join(ROOT, "gpurun_out", tag)
-    groups = defaultdict(lambda: {"calls": 0, "dur_ns": [], "fetch_kib": [], "write_kib": []})
-    for r in load(os.path.join(src, "ktrace", "kt_kernel_trace.csv")):
-        key = (r["Kernel_Name"], int(r["Grid_Size"]) if "Grid_Size" in r else int(r["Grid_Size_X"]))
-        g = groups[key]
-        g["calls"] += 1
-        g["dur_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    for sub, col in (("fetch", "fetch_kib"), ("write", "write_kib")):
-        d = os.path.join(src, sub)
-        f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
-        for r in load(os.path.join(d, f)):
-            groups[(r["Kernel_Name"], int(r["Grid_Size"]))][col].append(float(r["Counter_Value"]))
+def roles(n):
     out = []
-    for (name, grid), g in groups.items():
-        if "zfec_hip" not in name:
-            continue
+    for i in range(n):
+        if i == 0:
+            out.append("encode")
+        elif i < n - 2 * B2B:
+            out.append("encode" if (i - 1) % 2 == 0 else "decode")
+        else:
+            out.append("encode" if i < n - B2B else "decode")
+    return out
+
+
+def ours(rows):
+    rows = [r for r in rows if "zfec_hip" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0))
+    return rows
+
+
+def counter_rows(d):
+    f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
+    rows = ours(load(os.path.join(d, f)))
+    return rows
+
+
+def summarize(src):
+    kt = ours(load(os.path.join(src, "ktrace", "kt_kernel_trace.csv")))
+    fe = counter_rows(os.path.join(src, "fetch"))
+    wr = counter_rows(os.path.join(src, "write"))
+    res = {}
+    for rows, col in ((kt, "dur_ns"), (fe, "fetch_kib"), (wr, "write_kib")):
+        for r, role in zip(rows, roles(len(rows))):
+            e = res.setdefault(role, {"kernel": short(r["Kernel_Name"]), "dur_ns": [], "fetch_kib": [], "write_kib": []})
+            if col == "dur_ns":
+                e[col].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            else:
+                e[col].append(float(r["Counter_Value"]))
+    out = {}
+    for role, e in res.items():
         mean = lambda v: sum(v) / len(v) if v else None
-        fetch, write = mean(g["fetch_kib"]), mean(g["write_kib"])
-        traffic = None if fetch is None or write is None else 2 * fetch * 1024 + write * 1024
-        out.append({"kernel": short(name), "grid_threads": grid, "calls": g["calls"],
-                    "mean_us": round(mean(g["dur_ns"]) / 1e3, 3) if g["dur_ns"] else None,
-                    "fetch_kib_raw": fetch, "write_kib": write, "hbm_bytes_per_launch": traffic})
-    out.sort(key=lambda x: (x["kernel"], x["grid_threads"]))
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", tag + "_pmc.json"), "w") as f:
-        json.dump(out, f, indent=1)
-    shutil.copy(os.path.join(src, "ktrace", "kt_kernel_stats.csv"), os.path.join(ROOT, "profiles", tag + "_kernel_stats.csv"))
-    summ = {"source": "profiles/%s_pmc.json (tools/profile_round.sh %s)" % (tag, tag),
+        fetch, write = mean(e["fetch_kib"]), mean(e["write_kib"])
+        out[role] = {"kernel": e["kernel"], "launches": len(e["dur_ns"]),
+                     "mean_us": round(mean(e["dur_ns"]) / 1e3, 3) if e["dur_ns"] else None,
+                     "fetch_kib_raw": fetch, "write_kib": write,
+                     "hbm_bytes_per_launch": None if fetch is None or write is None else 2 * fetch * 1024 + write * 1024}
+    return out
+
+
+def main(tag):
+    base = os.path.join(ROOT, "gpurun_out", tag)
+    allw = {}
+    summ = {"source": "profiles/%s_pmc.json (tools/profile_round.sh %s; tools/pmc_summary.py %s)" % (tag, tag, tag),
             "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB*1024), MI355X_MICROARCH.md HBM section"}
-    for e in out:
-        if e["kernel"].startswith("matapply_reg<3, 7") and e["grid_threads"] == 1398272:
-            summ["encode_cfg2"] = e
-        if e["kernel"].startswith("matapply_reg<3, 3") and e["grid_threads"] == 1398272:
-            summ["decode_cfg2"] = e
+    for w in sorted(os.listdir(base)):
+        if not os.path.isdir(os.path.join(base, w, "ktrace")):
+            continue
+        allw[w] = summarize(os.path.join(base, w))
+        shutil.copy(os.path.join(base, w, "ktrace", "kt_kernel_stats.csv"),
+                    os.path.join(ROOT, "profiles", "%s_%s_kernel_stats.csv" % (tag, w)))
+        for role, e in allw[w].items():
+            summ["%s_%s" % (role, w)] = e
+            print(w, role, e)
+    with open(os.path.join(ROOT, "profiles", tag + "_pmc.json"), "w") as f:
+        json.dump(allw, f, indent=1)
     with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
         json.dump(summ, f, indent=1)
-    for e in out:
-        print(e)
 
 
 if __name__ == "__main__":
