@@ -23,8 +23,8 @@ scaling).  cfg4/cfg5: the fixed batch is split by zfec_amd.shard.shard_range
 max/sum reductions.
 
 Also reported: the dominant kernel's roofline (encode: (k+r)*sz*stripes
-algorithmic HBM bytes per launch / mean launch time, 20 back-to-back
-launches between HIP events on the launch stream; PMC traffic from
+algorithmic HBM bytes per launch / median launch time of 50 back-to-back
+launches with HIP events between them on the launch stream; PMC traffic from
 profiles/pmc_summary.json), the decode kernel's, a batched 1 MiB-stripe
 encode (the north-star shape), and a bounded CPU baseline (rank 0, N=1) of
 the reference's own C code (oracle/_ref, kind "reference") or the oracle
@@ -249,16 +249,18 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
     barrier(dist)
     el = time.perf_counter() - t0
 
-    # Per-kernel launch duration for the roofline: each kernel launched back to
-    # back on the same stream, bracketed by one pair of HIP events.
-    def b2b(fn, n=20):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(n):
+    # Per-kernel launch duration for the roofline: n launches back to back on
+    # the launch stream with a HIP event recorded between consecutive launches;
+    # the median of the n event-to-event intervals (robust to the first
+    # launch's start-up and to one-off stalls).
+    def b2b(fn, n=50):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        for i in range(n):
+            ev[i].record(stream)
             fn(stream.cuda_stream)
-        b.record(stream)
+        ev[n].record(stream)
         torch.cuda.synchronize()
-        return a.elapsed_time(b) / n
+        return float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(n)]))
 
     return {"elapsed_s": el, "gpu_step_ms": e0.elapsed_time(e1) / steps, "launch": launch,
             "enc_ms": b2b(enc), "dec_ms": b2b(dec), "nrec": nrec, "slots": slots}
@@ -340,7 +342,7 @@ def main():
                      "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),
                      "kernel": "%s (encode)" % capi.variant_name(k, r), "algorithmic_bytes_per_launch": enc_bytes,
                      "launch_ms": round(t["enc_ms"], 4),
-                     "timing": "20 back-to-back launches between two HIP events on the launch stream"},
+                     "timing": "median of 50 back-to-back launches, a HIP event between consecutive launches on the launch stream"},
         "decode_roofline": {"achieved": round(dec_ach, 1), "frac": round(dec_ach / HBM_PEAK_GBPS, 4),
                             "kernel": "%s (decode)" % capi.variant_name(k, nrec),
                             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4)},

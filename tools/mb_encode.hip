@@ -121,13 +121,12 @@ int main(int argc, char** argv) {
         } vs[] = {
             {"lds<8,4,4>", matapply_lds<false, true, 8, 4, 4>, false, true, 16},
             {"lds<8,2,4>", matapply_lds<false, true, 8, 2, 4>, false, true, 8},
-            {"lds<16,2,4>", matapply_lds<false, true, 16, 2, 4>, false, true, 8},
-            {"lds<8,2,8>", matapply_lds<false, true, 8, 2, 8>, false, true, 8},
+            {"lds<8,2,12>", matapply_lds<false, true, 8, 2, 12>, false, true, 8},
+            {"lds<8,2,16>", matapply_lds<false, true, 8, 2, 16>, false, true, 8},
+            {"lds<8,4,12>", matapply_lds<false, true, 8, 4, 12>, false, true, 16},
             {"lds<16,2,2>", matapply_lds<false, true, 16, 2, 2>, false, true, 8},
-            {"lds<4,4,8>", matapply_lds<false, true, 4, 4, 8>, false, true, 16},
-            {"lds<8,4,8>", matapply_lds<false, true, 8, 4, 8>, false, true, 16},
         };
-        const int shapes_all[][2] = {{10, 6}, {10, 4}, {5, 8}, {20, 40}, {20, 20}, {16, 16}, {32, 32}, {8, 8}, {3, 17}, {12, 12}};
+        const int shapes_all[][2] = {{10, 6}, {10, 4}, {5, 8}, {8, 8}, {12, 4}, {16, 8}, {20, 20}};
         std::vector<std::array<int, 2>> shapes;
         if (const char* e = getenv("MB_SHAPE")) {  // "k,r": one shape only (for counter runs)
             int a = 0, b = 0;

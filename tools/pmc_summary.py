@@ -10,8 +10,8 @@ Reads gpurun_out/<tag>/<workload>/{ktrace,fetch,write}/*.csv (rocprofv3
                                 (read by bench.py for roofline.traffic)
 
 Roles come from dispatch order, which bench.py fixes (run_workload): one
-encode, then (encode, decode) pairs for warmup + 3 + steps, then 20 encodes
-and 20 decodes back to back.  Encode and decode of one workload can be the
+encode, then (encode, decode) pairs for warmup + 3 + steps, then 50 encodes
+and 50 decodes back to back.  Encode and decode of one workload can be the
 same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes 6), so
 names alone do not tell them apart.
 
@@ -26,7 +26,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-B2B = 20
+B2B = 50
 
 
 def short(name):
