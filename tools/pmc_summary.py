@@ -10,8 +10,8 @@ Reads gpurun_out/<tag>/<workload>/{ktrace,fetch,write}/*.csv (rocprofv3
                                 (read by bench.py for roofline.traffic)
 
 Roles come from dispatch order, which bench.py fixes (run_workload): one
-encode, then (encode, decode) pairs for warmup + 3 + steps, then 50 encodes
-and 50 decodes back to back.  Encode and decode of one workload can be the
+encode, then (encode, decode) pairs: warmup + 3 + steps + 50 timed by
+per-launch events.  Encode and decode of one workload can be the
 same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes 6), so
 names alone do not tell them apart.
 
@@ -26,7 +26,6 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-B2B = 50
 
 
 def short(name):
@@ -40,15 +39,7 @@ def load(path):
 
 
 def roles(n):
-    out = []
-    for i in range(n):
-        if i == 0:
-            out.append("encode")
-        elif i < n - 2 * B2B:
-            out.append("encode" if (i - 1) % 2 == 0 else "decode")
-        else:
-            out.append("encode" if i < n - B2B else "decode")
-    return out
+    return ["encode" if i == 0 or (i - 1) % 2 == 0 else "decode" for i in range(n)]
 
 
 def ours(rows):
