@@ -112,6 +112,45 @@ int main(int argc, char** argv) {
             CK(hipFree(xout));
         }
     }
+    if (getenv("MB_BATCH")) {  // cfg5 shape: 1e6 stripes of K=3 x 1366 B, rows 1536 apart; U and grid cap
+        const int k = 3, r = 7;
+        const size_t sz = 1366, ld = 1536, ns = 1000000;
+        uint8_t *xin, *xout;
+        CK(hipMalloc(&xin, ns * k * ld));
+        CK(hipMalloc(&xout, ns * r * ld));
+        CK(hipMemset(xin, 0x5a, ns * k * ld));
+        struct V {
+            const char* name;
+            KernelFn fn;
+            int upl;
+        } vs[] = {{"reg<3,7> U1", matapply_reg<3, 7, true, 1>, 1}, {"reg<3,7> U2", matapply_reg<3, 7, true, 2>, 2},
+                  {"reg<3,7> U4", matapply_reg<3, 7, true, 4>, 4}};
+        std::vector<std::vector<float>> t(3 * 4);
+        const int gms[4] = {4, 16, 64, 1024};
+        for (int round = 0; round < 5; ++round)
+            for (int i = 0; i < 3; ++i)
+                for (int g = 0; g < 4; ++g) {
+                    const Variant saved = g_reg[3][7];
+                    g_reg[3][7] = Variant{vs[i].fn, vs[i].name, 0, true, vs[i].upl};
+                    g_grid_mult = gms[g];
+                    MatJob j = make_job(xin, xout, k, r, sz, ld);
+                    j.nstripes = ns;
+                    j.in_sstride = k * ld;
+                    j.out_sstride = r * ld;
+                    for (int b = 0; b < k; ++b) j.in[b] = xin + b * ld;
+                    for (int b = 0; b < r; ++b) j.out[b] = xout + b * ld;
+                    t[i * 4 + g].push_back(time_ms([&] { MatJob jj = j; CK(launch_matapply(jj, 0)); }, 5));
+                    g_reg[3][7] = saved;
+                }
+        for (int i = 0; i < 3; ++i)
+            for (int g = 0; g < 4; ++g) {
+                auto& v = t[i * 4 + g];
+                std::sort(v.begin(), v.end());
+                printf("BATCH %-12s gm=%4d median %8.4f ms  hbm %7.1f GB/s\n", vs[i].name, gms[g], v[2],
+                       double(k + r) * sz * ns / (v[2] * 1e-3) / 1e9);
+            }
+        return 0;
+    }
     if (getenv("MB_AB")) {  // interleaved A/B of general-kernel variants: 7 rounds, median (guide §5.4 rule 24)
         struct V {
             const char* name;
@@ -121,12 +160,9 @@ int main(int argc, char** argv) {
         } vs[] = {
             {"lds<8,4,4>", matapply_lds<false, true, 8, 4, 4>, false, true, 16},
             {"lds<8,2,4>", matapply_lds<false, true, 8, 2, 4>, false, true, 8},
-            {"lds<8,2,12>", matapply_lds<false, true, 8, 2, 12>, false, true, 8},
-            {"lds<8,2,16>", matapply_lds<false, true, 8, 2, 16>, false, true, 8},
-            {"lds<8,4,12>", matapply_lds<false, true, 8, 4, 12>, false, true, 16},
             {"lds<16,2,2>", matapply_lds<false, true, 16, 2, 2>, false, true, 8},
         };
-        const int shapes_all[][2] = {{10, 6}, {10, 4}, {5, 8}, {8, 8}, {12, 4}, {16, 8}, {20, 20}};
+        const int shapes_all[][2] = {{10, 6}, {10, 4}, {8, 8}, {20, 40}, {20, 20}, {3, 17}, {16, 16}};
         std::vector<std::array<int, 2>> shapes;
         if (const char* e = getenv("MB_SHAPE")) {  // "k,r": one shape only (for counter runs)
             int a = 0, b = 0;
@@ -158,7 +194,7 @@ int main(int argc, char** argv) {
                     Variant* slot = k <= kRegK && r <= kRegR ? &g_reg[k][r] : (r <= 8 ? &g_lds_narrow : &g_lds_wide);
                     const Variant saved = *slot;
                     *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1, vs[i].lds, vs[i].chunk};
-                    g_grid_mult = 16;
+                    g_grid_mult = getenv("MB_GM") ? atoi(getenv("MB_GM")) : 16;
                     MatJob j = make_job(xin, xout, k, r, bsz, bsz);
                     if (round == 0) CK(hipMemset(xout, 0, r * bsz));
                     t[i].push_back(time_ms([&] { MatJob jj = j; CK(launch_matapply(jj, 0)); }, 10));

@@ -522,7 +522,7 @@ Variant g_reg[kRegK + 1][kRegR + 1];
 Variant g_lds_fewin, g_lds_narrow, g_lds_wide, g_lds_acc;
 std::once_flag g_dispatch_once;
 int g_num_cu = 0;
-int g_grid_mult = 16;  // grid cap = CUs x resident blocks per CU x g_grid_mult
+int g_grid_mult = 1024;  // grid cap = CUs x resident blocks per CU x g_grid_mult (1024: ~one unit per lane; measured +9 % on 10^6 4 KiB stripes vs 16)
 
 template <int K, int R>
 void set_reg() {
@@ -596,8 +596,8 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
             nb = 1;
         v->max_blocks_per_cu = nb;
     }
-    // One 16-byte unit per lane up to 16x the resident capacity; beyond that a
-    // grid-stride loop (the 64 MiB config fits in a single pass).
+    // One unit per lane up to g_grid_mult x the resident capacity; beyond that
+    // a grid-stride loop.
     const uint64_t lanes = (total + v->units_per_lane - 1) / v->units_per_lane;
     const uint64_t need = (lanes + kBlock - 1) / kBlock;
     const uint64_t cap = static_cast<uint64_t>(g_num_cu) * v->max_blocks_per_cu * g_grid_mult;
