@@ -158,11 +158,12 @@ int main(int argc, char** argv) {
             bool ktab, lds;
             int chunk;
         } vs[] = {
-            {"lds<8,4,4>", matapply_lds<false, true, 8, 4, 4>, false, true, 16},
+            {"auto", nullptr, false, true, 8},
             {"lds<8,2,4>", matapply_lds<false, true, 8, 2, 4>, false, true, 8},
             {"lds<16,2,2>", matapply_lds<false, true, 16, 2, 2>, false, true, 8},
+            {"lds<8,4,4>", matapply_lds<false, true, 8, 4, 4>, false, true, 16},
         };
-        const int shapes_all[][2] = {{10, 6}, {10, 4}, {8, 8}, {20, 40}, {20, 20}, {3, 17}, {16, 16}};
+        const int shapes_all[][2] = {{10, 6}, {10, 4}, {8, 8}, {16, 6}, {20, 40}, {20, 20}, {16, 16}, {32, 32}, {12, 41}, {7, 13}, {32, 48}};
         std::vector<std::array<int, 2>> shapes;
         if (const char* e = getenv("MB_SHAPE")) {  // "k,r": one shape only (for counter runs)
             int a = 0, b = 0;
@@ -191,9 +192,9 @@ int main(int argc, char** argv) {
                 for (int i = 0; i < nv; ++i) {
                     if (vs[i].ktab && k * r > kMaxKernargTables) continue;
                     if (only && strcmp(only, vs[i].name)) continue;
-                    Variant* slot = k <= kRegK && r <= kRegR ? &g_reg[k][r] : (r <= 8 ? &g_lds_narrow : &g_lds_wide);
+                    Variant* slot = pick(k, r, false);
                     const Variant saved = *slot;
-                    *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1, vs[i].lds, vs[i].chunk};
+                    if (vs[i].fn) *slot = Variant{vs[i].fn, vs[i].name, 0, vs[i].ktab, 1, vs[i].lds, vs[i].chunk};
                     g_grid_mult = getenv("MB_GM") ? atoi(getenv("MB_GM")) : 16;
                     MatJob j = make_job(xin, xout, k, r, bsz, bsz);
                     if (round == 0) CK(hipMemset(xout, 0, r * bsz));
@@ -208,7 +209,7 @@ int main(int argc, char** argv) {
                 if (t[i].empty()) continue;
                 std::sort(t[i].begin(), t[i].end());
                 const double by = double(k + r) * bsz;
-                printf("AB k=%2d r=%2d %-10s median %8.4f ms  hbm %7.1f GB/s  input %7.1f GB/s\n", k, r, vs[i].name,
+                printf("AB k=%2d r=%2d %-10s median %8.4f ms  hbm %7.1f GB/s  input %7.1f GB/s\n", k, r, vs[i].fn ? vs[i].name : pick(k, r, false)->name,
                        t[i][3], by / (t[i][3] * 1e-3) / 1e9, double(k) * bsz / (t[i][3] * 1e-3) / 1e9);
             }
             CK(hipFree(xin));

@@ -34,6 +34,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 
@@ -293,12 +294,13 @@ struct LdsTab {
     u32x4 w4;   // c*{0,64,128,192}, 3 pad words (keeps both reads on one base address)
 };
 
-__device__ __forceinline__ void lds_tables_build(const MatJob& job, LdsTab* t) {
-    const uint32_t n = job.k * job.r;
+// Entry (input j, row) at j * rp + row, rp >= r: a tile's rows for one input
+// are adjacent; rows r..rp-1 (padding up to whole tiles) get the zero table.
+__device__ __forceinline__ void lds_tables_build(const MatJob& job, LdsTab* t, uint32_t rp) {
+    const uint32_t n = job.k * rp;
     for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-        // entry (input j, row) at j * r + row: a tile's rows for one input are adjacent
-        const uint32_t j = i / job.r, row = i - j * job.r;
-        const uint32_t c = job.coef[row * job.k + j];
+        const uint32_t j = i / rp, row = i - j * rp;
+        const uint32_t c = row < job.r ? job.coef[row * job.k + j] : 0u;
         const uint32_t* b = &g_bank.w[c * 8];
         t[i].w03 = u32x4{b[0], b[1], b[2], b[3]};
         t[i].w4 = u32x4{b[4], 0u, 0u, 0u};
@@ -374,13 +376,69 @@ struct Step {
     uint32_t rb, g;
 };
 
-template <bool ACC, bool NT, int RT_, int D, int GG>
-__global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
+// acc[rr] ^= sum over the group's inputs of table(j, rb + rr) * x_j, for the
+// RT_ rows of one tile.  FULL: every row of the tile exists (no per-row
+// branch, so no register copies where the two paths of a branch meet).
+template <bool FULL, int RT_, int D, int GG>
+__device__ __forceinline__ void mac_group(uint32_t (&a)[RT_][D], const Words<D> (&x)[GG], const LdsTab* lds_tab,
+                                          uint32_t g, uint32_t rb, uint32_t k, uint32_t r) {
+#pragma unroll
+    for (int jj = 0; jj < GG; jj += 2) {
+        const uint32_t j = g + jj;
+        if (j >= k) break;
+        Sel s0[D];
+#pragma unroll
+        for (int v = 0; v < D; ++v) s0[v] = selectors(x[jj].w[v]);
+        const LdsTab* t0 = lds_tab + j * r + rb;
+        if (jj + 1 < GG && j + 1 < k) {  // two inputs: their six partial products share three XOR3s
+            Sel s1[D];
+#pragma unroll
+            for (int v = 0; v < D; ++v) s1[v] = selectors(x[jj + 1].w[v]);
+            const LdsTab* t1 = t0 + r;
+#pragma unroll
+            for (int rr = 0; rr < RT_; ++rr) {
+                if (FULL || rb + rr < r) {  // wave-uniform
+                    const u32x4 p = t0[rr].w03, q = t1[rr].w03;
+                    const uint32_t pu = t0[rr].w4.x, qu = t1[rr].w4.x;
+#pragma unroll
+                    for (int v = 0; v < D; ++v) a[rr][v] = gf_mac2(a[rr][v], p, pu, s0[v], q, qu, s1[v]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int rr = 0; rr < RT_; ++rr) {
+                if (FULL || rb + rr < r) {
+                    const u32x4 p = t0[rr].w03;
+                    const uint32_t pu = t0[rr].w4.x;
+#pragma unroll
+                    for (int v = 0; v < D; ++v) a[rr][v] = gf_mac_v(a[rr][v], p, pu, s0[v]);
+                }
+            }
+        }
+    }
+}
+
+// Row tiling of a launch, fixed by the dispatcher:
+enum TileMode {
+    kTilesRagged = 0,  // rows past r in the last tile are skipped by a per-row branch
+    kTilesPadded = 1,  // the table has zero rows up to whole tiles: no branch in the
+                       // multiply-accumulate, only the stores of padding rows are skipped
+};
+
+// Rows of the LDS table: r, or r rounded up to whole RT-row tiles.
+template <int MODE>
+__host__ __device__ constexpr uint32_t table_rows(uint32_t r, uint32_t rt) {
+    return MODE == kTilesPadded ? (r + rt - 1) / rt * rt : r;
+}
+
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE>
+__device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     constexpr uint32_t CH = 4 * D;
     extern __shared__ LdsTab lds_tab[];
     const uint32_t k = job.k;
     const uint32_t r = job.r;
-    lds_tables_build(job, lds_tab);
+    const uint32_t rp = table_rows<MODE>(r, RT_);
+    lds_tables_build(job, lds_tab, rp);
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / CH);
     // The walk visits, for each of this lane's units in grid-stride order, each
@@ -396,17 +454,18 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
             if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
     };
     Step cur{UnitIter(job), 0u, 0u};
-    const bool live0 = cur.u.s < job.nstripes;
-    Words<D> xa[GG];
-    if (live0) load_step(cur, xa);
+    bool live = cur.u.s < job.nstripes;
     uint32_t a[RT_][D];
 #pragma unroll
     for (int rr = 0; rr < RT_; ++rr)
 #pragma unroll
         for (int v = 0; v < D; ++v) a[rr][v] = 0u;
-    // Every lane walks the same (rb, g) sequence; a lane whose units ran out
-    // keeps stepping (without memory traffic) until the whole wave is done.
-    bool live = live0;
+    // One step: prefetch the next step's group into xb, compute the current
+    // group from xa, store the tile when its last group is done.  Every lane
+    // walks the same (rb, g) sequence; a lane whose units ran out keeps
+    // stepping (without memory traffic) until the whole wave is done.
+    Words<D> xa[GG];
+    if (live) load_step(cur, xa);
     while (__any(live)) {
         Step nxt = cur;
         nxt.g += GG;
@@ -423,58 +482,23 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
         Words<D> xb[GG];
         if (nlive) load_step(nxt, xb);
         if (live) {
-#pragma unroll
-            for (int jj = 0; jj < GG; jj += 2) {
-                const uint32_t j = cur.g + jj;
-                if (j >= k) break;
-                Sel s0[D];
-#pragma unroll
-                for (int v = 0; v < D; ++v) s0[v] = selectors(xa[jj].w[v]);
-                const LdsTab* t0 = lds_tab + j * r + cur.rb;
-                if (j + 1 < k) {  // two inputs: their six partial products share three XOR3s
-                    Sel s1[D];
-#pragma unroll
-                    for (int v = 0; v < D; ++v) s1[v] = selectors(xa[jj + 1].w[v]);
-                    const LdsTab* t1 = t0 + r;
-#pragma unroll
-                    for (int rr = 0; rr < RT_; ++rr) {
-                        if (cur.rb + rr < r) {  // wave-uniform
-                            const u32x4 p = t0[rr].w03, q = t1[rr].w03;
-                            const uint32_t pu = t0[rr].w4.x, qu = t1[rr].w4.x;
-#pragma unroll
-                            for (int v = 0; v < D; ++v) a[rr][v] = gf_mac2(a[rr][v], p, pu, s0[v], q, qu, s1[v]);
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int rr = 0; rr < RT_; ++rr) {
-                        if (cur.rb + rr < r) {
-                            const u32x4 p = t0[rr].w03;
-                            const uint32_t pu = t0[rr].w4.x;
-#pragma unroll
-                            for (int v = 0; v < D; ++v) a[rr][v] = gf_mac_v(a[rr][v], p, pu, s0[v]);
-                        }
-                    }
-                }
-            }
+            mac_group<MODE == kTilesPadded, RT_, D, GG>(a, xa, lds_tab, cur.g, cur.rb, k, rp);
             if (tile_end) {
                 const Span sp = chunk_span<CH, !ACC>(cur.u.c, sz, nfull);
                 const uint64_t ob = cur.u.s * job.out_sstride + sp.off;
-                const bool full = sp.full;
-                const uint32_t nb = sp.nb;
 #pragma unroll
                 for (int rr = 0; rr < RT_; ++rr) {
-                    if (cur.rb + rr >= r) continue;
+                    if (cur.rb + rr >= r) continue;  // ragged tail or padding rows
                     uint8_t* op = job.out[cur.rb + rr] + ob;
                     Words<D> y;
 #pragma unroll
                     for (int v = 0; v < D; ++v) y.w[v] = a[rr][v];
                     if constexpr (ACC) {
-                        const Words<D> o = load_words<D>(op, full, nb);
+                        const Words<D> o = load_words<D>(op, sp.full, sp.nb);
 #pragma unroll
                         for (int v = 0; v < D; ++v) y.w[v] ^= o.w[v];
                     }
-                    store_words<D, NT>(op, y, full, nb);
+                    store_words<D, NT>(op, y, sp.full, sp.nb);
                 }
             }
         }
@@ -491,6 +515,11 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
     }
 }
 
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE = kTilesRagged>
+__global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
+    matapply_lds_body<ACC, NT, RT_, D, GG, MODE>(job);
+}
+
 // ---------------------------------------------------------------------------
 // Dispatch
 // ---------------------------------------------------------------------------
@@ -504,6 +533,7 @@ struct Variant {
     int units_per_lane = 1; // units a lane handles per loop trip (grid sizing)
     bool lds_tables = false; // dynamic LDS of 32 bytes per coefficient
     int chunk = kChunk;      // bytes per unit (a lane's slice of one block)
+    int pad_tile = 0;        // kTilesPadded: rows per tile (the LDS table is padded to whole tiles)
 };
 
 // Register-table variants: k <= 4, r <= 8.
@@ -519,7 +549,13 @@ const char* const kRegNames[kRegK + 1][kRegR + 1] = {
     {"", "matapply_reg<4,1>", "matapply_reg<4,2>", "matapply_reg<4,3>", "matapply_reg<4,4>", "matapply_reg<4,5>",
      "matapply_reg<4,6>", "matapply_reg<4,7>", "matapply_reg<4,8>"}};
 Variant g_reg[kRegK + 1][kRegR + 1];
-Variant g_lds_fewin, g_lds_narrow, g_lds_wide, g_lds_acc;
+Variant g_lds_fewin, g_lds_acc;
+// Padded-tile variants by tile height: 1-8 rows in one tile (r <= 8), 9-20
+// rows for wider codes split into ceil(r/20) near-equal tiles.
+constexpr int kMaxTile = 20;
+// Largest table: k = 32 inputs x (48 rows + up to 2 padding rows).
+constexpr int kMaxLdsTables = kMaxIn * (kMaxOut + 2);
+Variant g_lds_pad[kMaxTile + 1];
 std::once_flag g_dispatch_once;
 int g_num_cu = 0;
 int g_grid_mult = 1024;  // grid cap = CUs x resident blocks per CU x g_grid_mult (1024: ~one unit per lane; measured +9 % on 10^6 4 KiB stripes vs 16)
@@ -541,18 +577,27 @@ void fill_reg_row() {
     set_reg<K, 8>();
 }
 
+template <int RT>
+void fill_pad() {
+    static char name[40];
+    constexpr int G = (RT <= 4 || RT == 8) ? 4 : 2;  // input group size: measured per tile height
+    snprintf(name, sizeof name, "matapply_lds<%d,2,%d,pad>", RT, G);
+    g_lds_pad[RT] = Variant{matapply_lds<false, true, RT, 2, G, kTilesPadded>, name, 0, false, 1, true, 8, RT};
+    if constexpr (RT < kMaxTile) fill_pad<RT + 1>();
+}
+
 void init_dispatch() {
     fill_reg_row<1>();
     fill_reg_row<2>();
     fill_reg_row<3>();
     fill_reg_row<4>();
-    // measured (tools/mb_encode.exe MB_AB): k <= 4 (memory-bound) takes 16
-    // bytes per lane in 8-row tiles; otherwise 8 bytes per lane, 8-row tiles
-    // with 4-input groups for r <= 8, 16-row tiles with 2-input groups above
+    // measured (tools/mb_encode.exe MB_AB, interleaved medians): k <= 4
+    // (memory-bound) takes 16 bytes per lane in ragged 8-row tiles; wider
+    // codes take 8 bytes per lane in padded tiles (no per-row branches), as
+    // few tiles as 20-row register tiles allow (inputs are re-read per tile)
     g_lds_fewin = Variant{matapply_lds<false, true, 8, 4, 4>, "matapply_lds<8,4,4>", 0, false, 1, true, 16};
-    g_lds_narrow = Variant{matapply_lds<false, true, 8, 2, 4>, "matapply_lds<8,2,4>", 0, false, 1, true, 8};
-    g_lds_wide = Variant{matapply_lds<false, true, 16, 2, 2>, "matapply_lds<16,2,2>", 0, false, 1, true, 8};
     g_lds_acc = Variant{matapply_lds<true, false, 16, 2, 2>, "matapply_lds<16,2,2,acc>", 0, false, 1, true, 8};
+    fill_pad<1>();
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) {
         hipDeviceProp_t prop;
@@ -567,7 +612,8 @@ Variant* pick(uint32_t k, uint32_t r, bool acc) {
     if (acc) return &g_lds_acc;
     if (k >= 1 && k <= static_cast<uint32_t>(kRegK) && r >= 1 && r <= static_cast<uint32_t>(kRegR)) return &g_reg[k][r];
     if (k <= 4) return &g_lds_fewin;
-    return r <= 8 ? &g_lds_narrow : &g_lds_wide;
+    const uint32_t tiles = (r + kMaxTile - 1) / kMaxTile;
+    return &g_lds_pad[(r + tiles - 1) / tiles];
 }
 
 }  // namespace
@@ -586,11 +632,12 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     if (total >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits larger jobs
     job.cps = static_cast<uint32_t>(cps);
 
-    const size_t lds = v->lds_tables ? size_t(job.k) * job.r * 32 : 0;
+    const size_t rows = v->pad_tile ? (job.r + v->pad_tile - 1) / v->pad_tile * v->pad_tile : job.r;
+    const size_t lds = v->lds_tables ? size_t(job.k) * rows * 32 : 0;
     if (v->max_blocks_per_cu == 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v->fn), kBlock,
-                                                         v->lds_tables ? kMaxCoef * 32 : 0) !=
+                                                         v->lds_tables ? kMaxLdsTables * 32 : 0) !=
                 hipSuccess ||
             nb <= 0)
             nb = 1;
