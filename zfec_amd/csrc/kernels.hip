@@ -467,6 +467,10 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     Words<D> xa[GG];
     if (live) load_step(cur, xa);
     while (__any(live)) {
+        // (g, rb) are wave-uniform; say so, or they live in VGPRs and every
+        // block pointer becomes a readfirstlane + dependent scalar load.
+        cur.g = __builtin_amdgcn_readfirstlane(cur.g);
+        cur.rb = __builtin_amdgcn_readfirstlane(cur.rb);
         Step nxt = cur;
         nxt.g += GG;
         const bool tile_end = nxt.g >= k;
