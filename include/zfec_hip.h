@@ -86,7 +86,7 @@ enum {
     FEC_EUNINIT = 6     /* fec_init() not called */
 };
 
-#define FEC_FLAG_ASYNC 1u          /* do not synchronize; all buffers must be device memory */
+#define FEC_FLAG_ASYNC 1u          /* do not synchronize; all buffers device or page-locked host memory */
 #define FEC_FLAG_LIBRARY_STREAM 2u /* ignore `stream`; use the library's per-thread stream */
 
 /* Status of the last library call made by this thread, and its message. */
@@ -97,8 +97,13 @@ const char* fec_last_error_message(void);
  * `stream` follows HIP's convention: NULL is the null (legacy default) stream,
  * which is what torch's default stream hands out.  FEC_FLAG_LIBRARY_STREAM
  * selects the library's own per-thread non-blocking stream instead (what the
- * synchronous fec_encode / fec_decode use).  With FEC_FLAG_ASYNC and device
- * buffers the call only enqueues work on the stream. */
+ * synchronous fec_encode / fec_decode use).  With FEC_FLAG_ASYNC and device or
+ * page-locked host buffers the call only enqueues work on the stream.
+ *
+ * Host buffers: page-locked ones (fec_host_alloc, hipHostMalloc,
+ * hipHostRegister) are read and written by the kernel in place over PCIe;
+ * large pageable ones are page-locked for the duration of the call and then
+ * treated the same way; small pageable ones go through a bounce buffer. */
 int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fecs,
                   const unsigned* block_nums, size_t num_block_nums, size_t sz,
                   void* stream, unsigned flags);
@@ -106,7 +111,7 @@ int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts
                   const unsigned* index, size_t sz, void* stream, unsigned flags);
 
 /* Batched encode of nstripes independent stripes in one launch (device memory
- * only).  Block j of stripe s is read from src + s*src_stripe_stride +
+ * on one device, or page-locked host memory).  Block j of stripe s is read from src + s*src_stripe_stride +
  * j*src_block_stride; output i of stripe s (block block_nums[i]) is written to
  * dst + s*dst_stripe_stride + i*dst_block_stride.  Packed [stripe][block][sz]
  * layouts use block_stride = sz, stripe_stride = k*sz (input) / num*sz (output). */
@@ -126,10 +131,9 @@ int fec_decode_batch(const fec_t* code,
                      const unsigned* index, size_t sz, size_t nstripes,
                      void* stream, unsigned flags);
 
-/* Page-locked host memory on the current device's node (hipHostMalloc): host
- * buffers passed to fec_encode / fec_decode from here are DMA'd in place by
- * the overlapped H2D / kernel / D2H pipeline (no per-call pinning).  NULL on
- * failure (status set). */
+/* Page-locked host memory (hipHostMalloc): host buffers passed to fec_encode /
+ * fec_decode from here are read and written by the kernel in place (no
+ * per-call pinning, no staging copies).  NULL on failure (status set). */
 void* fec_host_alloc(size_t bytes);
 void fec_host_free(void* p);
 

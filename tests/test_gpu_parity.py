@@ -224,6 +224,84 @@ def test_c_abi_host_pointers():
     assert (rec == data[[0, 2, 4]]).all()
 
 
+def _encode_ptrs_check(code, k, m, data, in_addrs, out_addrs, read_out, sz):
+    code.encode_ptrs(in_addrs, out_addrs, list(range(k, m)), sz, flags=0)
+    got = read_out()
+    assert (got == oracle.encode(k, m, data)).all()
+
+
+def test_c_abi_large_pageable_host_blocks_sharing_pages():
+    """> 4 MiB of pageable host blocks: page-locked for the call (ranges that
+    share pages merged) and read / written by the kernel in place."""
+    k, m = 3, 10
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(17)
+    for sz in [2_500_001, 1 << 21]:
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        buf = np.zeros(k * sz + 11, dtype=np.uint8)  # blocks back to back at an odd offset: neighbours share pages
+        buf[5:5 + k * sz] = data.reshape(-1)
+        obuf = np.zeros((m - k) * sz + 11, dtype=np.uint8)
+        base, obase = buf.ctypes.data + 5, obuf.ctypes.data + 3
+        _encode_ptrs_check(code, k, m, data, [base + j * sz for j in range(k)], [obase + i * sz for i in range(m - k)],
+                           lambda: obuf[3:3 + (m - k) * sz].reshape(m - k, sz), sz)
+        assert obuf[:3].sum() == 0 and obuf[3 + (m - k) * sz:].sum() == 0
+
+
+def test_c_abi_pinned_and_mixed_blocks():
+    """Page-locked host blocks (fec_host_alloc) are used in place; any mix of
+    device, pinned and pageable blocks in one call."""
+    k, m = 4, 9
+    code = capi.Code(k, m)
+    L = capi.lib()
+    rng = np.random.default_rng(23)
+    for sz in [100, 333_333, 3_000_000]:
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        want = oracle.encode(k, m, data)
+        pins = [L.fec_host_alloc(sz) for _ in range(k + m - k)]
+        try:
+            arrs = [np.ctypeslib.as_array((ctypes.c_ubyte * sz).from_address(p)) for p in pins]
+            for j in range(k):
+                arrs[j][:] = data[j]
+            # all pinned
+            _encode_ptrs_check(code, k, m, data, pins[:k], pins[k:], lambda: np.stack(arrs[k:]), sz)
+            # mixed: input 0 on the device, input 1 pageable, outputs alternate pinned / device / pageable
+            dev_in = torch.from_numpy(data[0].copy()).cuda()
+            page_in = data[1].copy()
+            dev_out = torch.zeros(sz, dtype=torch.uint8, device="cuda")
+            page_out = np.zeros(sz, dtype=np.uint8)
+            ins = [dev_in.data_ptr(), page_in.ctypes.data, pins[2], pins[3]]
+            for a in arrs[k:]:
+                a[:] = 0
+            outs = [pins[k], dev_out.data_ptr(), page_out.ctypes.data, pins[k + 3], pins[k + 4]]
+            code.encode_ptrs(ins, outs, list(range(k, m)), sz, flags=0)
+            torch.cuda.synchronize()
+            assert (arrs[k] == want[0]).all() and (dev_out.cpu().numpy() == want[1]).all()
+            assert (page_out == want[2]).all() and (arrs[k + 3] == want[3]).all() and (arrs[k + 4] == want[4]).all()
+        finally:
+            for p in pins:
+                L.fec_host_free(p)
+
+
+def test_batch_pinned_host():
+    """fec_encode_batch / fec_decode_batch on page-locked host memory."""
+    k, m, sz, ns = 3, 10, 4096, 300
+    code = capi.Code(k, m)
+    L = capi.lib()
+    rng = np.random.default_rng(29)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    p_in, p_out = L.fec_host_alloc(data.nbytes), L.fec_host_alloc(ns * (m - k) * sz)
+    try:
+        a_in = np.ctypeslib.as_array((ctypes.c_ubyte * data.nbytes).from_address(p_in)).reshape(ns, k, sz)
+        a_out = np.ctypeslib.as_array((ctypes.c_ubyte * (ns * (m - k) * sz)).from_address(p_out)).reshape(ns, m - k, sz)
+        a_in[:] = data
+        code.encode_batch(p_in, sz, k * sz, p_out, sz, (m - k) * sz, list(range(k, m)), sz, ns, flags=0)
+        for s in [0, 1, ns // 2, ns - 1]:
+            assert (a_out[s] == oracle.encode(k, m, data[s])).all(), s
+    finally:
+        L.fec_host_free(p_in)
+        L.fec_host_free(p_out)
+
+
 def test_c_abi_device_pointers_misaligned():
     code = capi.Code(3, 10)
     rng = np.random.default_rng(11)
