@@ -88,6 +88,8 @@ enum {
 
 #define FEC_FLAG_ASYNC 1u          /* do not synchronize; all buffers device or page-locked host memory */
 #define FEC_FLAG_LIBRARY_STREAM 2u /* ignore `stream`; use the library's per-thread stream */
+#define FEC_FLAG_ALL_PRIMARIES 4u  /* decode: output all k primaries in order (present ones copied),
+                                      not only the missing ones: the output is the stripe itself */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);

@@ -363,6 +363,24 @@ def test_batch_encode_decode(k, m, sz, ns):
     assert (rec.cpu().numpy() == data[:, missing, :]).all()
 
 
+@pytest.mark.parametrize("k,m,nums", [(3, 10, [7, 1, 9]), (5, 9, [0, 1, 2, 3, 4]), (10, 16, list(range(6, 16)))])
+def test_decode_all_primaries_flag(k, m, nums):
+    """FEC_FLAG_ALL_PRIMARIES: the k outputs are the primaries in order, present ones copied."""
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(k * m)
+    sz, ns = 999, 7
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    allb = np.concatenate([data, np.stack([oracle.encode(k, m, data[s]) for s in range(ns)])], axis=1)
+    slots = place(nums, k)
+    recv = torch.from_numpy(np.ascontiguousarray(allb[:, slots, :])).cuda()
+    out = torch.zeros((ns, k, sz), dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr(), sz, k * sz, out.data_ptr(), sz, k * sz, slots, sz, ns,
+                      stream=torch.cuda.current_stream().cuda_stream,
+                      flags=capi.FEC_FLAG_ASYNC | capi.FEC_FLAG_ALL_PRIMARIES)
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == data).all()
+
+
 # ---- BASELINE config sizes ------------------------------------------------------
 
 def test_config2_64mib_vs_oracle():

@@ -500,7 +500,11 @@ int check_block_nums(const fec_t* code, const unsigned* nums, size_t num) {
 }
 
 // Rows of the decode matrix for the missing primaries (ascending), r x k.
-int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& rows, unsigned& r) {
+// The decode matrix rows to apply: the missing primaries' (ascending), or with
+// all_primaries every primary's (a present primary's row is a unit vector:
+// the output is a copy, so the k outputs are the stripe in order).
+int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& rows, unsigned& r,
+                bool all_primaries = false) {
     const unsigned k = code->k;
     if (!index) return set_status(FEC_EINVAL, "index is NULL");
     std::vector<unsigned char> seen(256, 0);
@@ -518,7 +522,7 @@ int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& 
     rows.clear();
     r = 0;
     for (unsigned i = 0; i < k; ++i) {
-        if (index[i] < k) continue;
+        if (index[i] < k && !all_primaries) continue;
         rows.insert(rows.end(), dec.begin() + size_t(i) * k, dec.begin() + size_t(i + 1) * k);
         ++r;
     }
@@ -606,7 +610,7 @@ FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const*
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
     std::vector<uint8_t> rows;
     unsigned r = 0;
-    if (decode_rows(code, index, rows, r)) return t_status;
+    if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0) return set_status(FEC_OK);
     if (!inpkts || !outpkts) return set_status(FEC_EINVAL, "NULL block array");
     return run_single(rows.data(), code->k, r, inpkts, outpkts, sz, stream, flags);
@@ -734,7 +738,7 @@ FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
     std::vector<uint8_t> rows;
     unsigned r = 0;
-    if (decode_rows(code, index, rows, r)) return t_status;
+    if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
     return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
                      dst_stripe_stride, sz, nstripes, stream, flags);

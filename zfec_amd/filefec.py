@@ -10,16 +10,15 @@ the reference itself).
 The reference encodes a file segment by segment: each segment is k*4096
 input bytes split easyfec-style into k blocks, and share i is the header
 followed by block i of every segment.  Here a window of W whole segments is
-one GPU call: the window is regrouped block-major ([k][W*4096]; block j of
-the window = block j of every segment, back to back), so ONE encode of k
-blocks of W*4096 bytes yields the m share bodies of the window directly --
-parity rows for i >= k, and the regrouped input rows for i < k.  Decoding is
-the same in reverse: W*4096 bytes of each of k shares are the k blocks of
-one call, and the recovered rows are regrouped segment-major for the output.
-Window buffers are pinned (fec_host_alloc), so the library streams them
-through its overlapped H2D / kernel / D2H pipeline.  Only the final, short
-segment takes the per-segment path.
+one batched GPU call (stripe = segment): it reads the window as the file lays
+it out and writes the m share bodies of the window block-major, so each share
+file gets one contiguous write per window.  Decoding: W*4096 bytes of each
+of k shares are the k blocks of one call, and the recovered rows are
+regrouped segment-major for the output.  Window buffers are page-locked
+(fec_host_alloc), so the kernel reads and writes them in place over PCIe.
+Only the final, short segment takes the per-segment path.
 """
+import itertools
 import os
 import struct
 
@@ -218,15 +217,35 @@ def encode_to_files(inf, fsize, dirname, prefix, k, m, suffix=".fec", overwrite=
 
 
 def _encode_stream(inf, fsize, k, m, fs, verbose):
+    """Whole segments go through the GPU a window at a time: ONE batched call
+    per window reads the window as the file lays it out (segment-major, stripe
+    = segment, block j of segment s at s*k*4096 + j*4096) and writes all m
+    share rows block-major (row i = block i of every segment; rows i < k are
+    copies of the primaries), so each share file gets one contiguous write.
+    Both buffers are page-locked, so the kernel reads and writes them in place.
+    Two window buffers alternate: while one window's m share writes run (a
+    thread pool, one file per task), the next window is read and encoded; a
+    window's writes start only after the previous window's have finished, so
+    every file is written in order."""
+    from concurrent.futures import ThreadPoolExecutor
+
     seg = k * CHUNKSIZE
     wseg = max(1, WINDOW_BYTES // seg)
     code = capi.Code(k, m)
-    win_in = _PinnedArray(wseg * seg)           # segment-major, as read from the file
-    rows = _PinnedArray(wseg * seg)             # block-major regrouping of win_in
-    par = _PinnedArray((m - k) * wseg * CHUNKSIZE) if m > k else None
+    nums = list(range(m))
+    bufs = [(_PinnedArray(wseg * seg), _PinnedArray(m * wseg * CHUNKSIZE)) for _ in range(2)]
+    pool = ThreadPoolExecutor(max_workers=min(m, 8))
+    pending = []  # the previous window's writes
+
+    def drain():
+        for fut in pending:
+            fut.result()
+        del pending[:]
+
     total = 0
     try:
-        while True:
+        for it in itertools.count():
+            win_in, rows = bufs[it % 2]  # its writes (two windows ago) were drained before the last submit
             got = _readinto_full(inf, memoryview(win_in.array)[:wseg * seg])
             if got == 0:
                 break
@@ -237,18 +256,14 @@ def _encode_stream(inf, fsize, k, m, fs, verbose):
             nfull = got // seg
             if nfull:
                 w = nfull * CHUNKSIZE  # bytes per share in this window
-                blk = rows.array[:k * w].reshape(k, nfull, CHUNKSIZE)
-                blk[...] = win_in.array[:nfull * seg].reshape(nfull, k, CHUNKSIZE).transpose(1, 0, 2)
-                if m > k:
-                    code.encode_ptrs([rows.ptr + j * w for j in range(k)],
-                                     [par.ptr + i * w for i in range(m - k)], list(range(k, m)), w,
-                                     flags=capi.FEC_FLAG_LIBRARY_STREAM)
-                for i in range(k):
-                    fs[i].write(memoryview(rows.array)[i * w:(i + 1) * w])
-                for i in range(m - k):
-                    fs[k + i].write(memoryview(par.array)[i * w:(i + 1) * w])
+                code.encode_batch(win_in.ptr, CHUNKSIZE, seg, rows.ptr, w, CHUNKSIZE, nums, CHUNKSIZE, nfull,
+                                  flags=capi.FEC_FLAG_LIBRARY_STREAM)
+                drain()
+                view = memoryview(rows.array)
+                pending.extend(pool.submit(fs[i].write, view[i * w:(i + 1) * w]) for i in range(m))
             rest = got - nfull * seg
             if rest:  # the final, short segment: easyfec split/pad, as the reference does
+                drain()
                 tail = bytes(win_in.array[nfull * seg:got])
                 for i, b in enumerate(easyfec.Encoder(k, m).encode(tail)):
                     fs[i].write(b)
@@ -256,9 +271,11 @@ def _encode_stream(inf, fsize, k, m, fs, verbose):
                 print("%d%% ..." % (100 * total // max(1, fsize)), end=" ")
             if got < wseg * seg:
                 break
+        drain()
     finally:
-        for a in (win_in, rows, par):
-            if a is not None:
+        pool.shutdown(wait=True)
+        for pair in bufs:
+            for a in pair:
                 a.free()
 
 
@@ -304,19 +321,27 @@ def decode_from_files(outf, infiles, verbose=False):
     it = iter(rest)
     slots = [s if s is not None else next(it) for s in slots]
     slot_nums = [shnums[i] for i in slots]
-    missing = [j for j in range(k) if slot_nums[j] >= k]
+
+    # One batched call per window: stripe = segment, slot j of segment s at
+    # ins + j*w_max + s*4096 (the window of share slots[j]); all k primaries
+    # come out segment-major, i.e. in file order (FEC_FLAG_ALL_PRIMARIES: a
+    # present primary's row is a copy).  Two window buffers alternate, so the
+    # output write of one window overlaps the share reads (one thread per
+    # share) and the decode of the next.
+    from concurrent.futures import ThreadPoolExecutor
 
     wseg = max(1, WINDOW_BYTES // (k * CHUNKSIZE))
     code = capi.Code(k, m)
     w_max = wseg * CHUNKSIZE
-    ins = _PinnedArray(k * w_max)
-    rec = _PinnedArray(max(1, len(missing)) * w_max)
-    outbuf = _PinnedArray(k * w_max)
+    bufs = [(_PinnedArray(k * w_max), _PinnedArray(k * w_max)) for _ in range(2)]
+    pool = ThreadPoolExecutor(max_workers=min(k, 8) + 1)
+    pending = []  # the previous window's output write
     byteswritten = 0
     try:
-        while True:
-            lens = [_readinto_full(infs[slots[j]], memoryview(ins.array)[j * w_max:(j + 1) * w_max])
-                    for j in range(k)]
+        for it in itertools.count():
+            ins, outbuf = bufs[it % 2]
+            lens = list(pool.map(lambda j: _readinto_full(infs[slots[j]],
+                                                          memoryview(ins.array)[j * w_max:(j + 1) * w_max]), range(k)))
             if any(n != lens[-1] for n in lens):
                 raise CorruptedShareFilesError(
                     "Share files were corrupted -- all share files are required to be the same length, but they "
@@ -326,19 +351,16 @@ def decode_from_files(outf, infiles, verbose=False):
                 break
             nfull, tail = divmod(n, CHUNKSIZE)
             if nfull:
-                w = nfull * CHUNKSIZE
-                if missing:
-                    code.decode_ptrs([ins.ptr + j * w_max for j in range(k)],
-                                     [rec.ptr + i * w_max for i in range(len(missing))], slot_nums, w,
-                                     flags=capi.FEC_FLAG_LIBRARY_STREAM)
-                out = outbuf.array[:nfull * k * CHUNKSIZE].reshape(nfull, k, CHUNKSIZE)
-                for j in range(k):
-                    src = ins.array[j * w_max:j * w_max + w] if slot_nums[j] < k else \
-                        rec.array[missing.index(j) * w_max:missing.index(j) * w_max + w]
-                    out[:, j, :] = src.reshape(nfull, CHUNKSIZE)
-                outf.write(memoryview(outbuf.array)[:nfull * k * CHUNKSIZE])
+                code.decode_batch(ins.ptr, w_max, CHUNKSIZE, outbuf.ptr, CHUNKSIZE, k * CHUNKSIZE, slot_nums,
+                                  CHUNKSIZE, nfull, flags=capi.FEC_FLAG_LIBRARY_STREAM | capi.FEC_FLAG_ALL_PRIMARIES)
+                for fut in pending:
+                    fut.result()
+                pending = [pool.submit(outf.write, memoryview(outbuf.array)[:nfull * k * CHUNKSIZE])]
                 byteswritten += nfull * k * CHUNKSIZE
             if tail:  # the final, short segment of each share
+                for fut in pending:
+                    fut.result()
+                pending = []
                 blocks = [bytes(ins.array[j * w_max + nfull * CHUNKSIZE:j * w_max + n]) for j in range(k)]
                 data = b"".join(zfec_amd.Decoder(k, m).decode(blocks, slot_nums))
                 outf.write(data)
@@ -347,9 +369,13 @@ def decode_from_files(outf, infiles, verbose=False):
                 print(str(byteswritten // 10 ** 6) + " MB ...", end=" ")
             if n < w_max:
                 break
+        for fut in pending:
+            fut.result()
     finally:
-        for a in (ins, rec, outbuf):
-            a.free()
+        pool.shutdown(wait=True)
+        for pair in bufs:
+            for a in pair:
+                a.free()
     if padlen:
         outf.truncate(byteswritten - padlen)
     if verbose:
