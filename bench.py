@@ -44,6 +44,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import zfec_amd  # noqa: E402
 from zfec_amd import capi  # noqa: E402
 from zfec_amd.shard import shard_range  # noqa: E402
 
@@ -178,6 +179,35 @@ def cpu_baseline(seconds, k, m, sz):
                           steps, k, m, k * sz, el,
                           "reference zfec/fec.c+_fecmodule.c compiled by oracle/Makefile (-O2 -march=x86-64-v2)"
                           if kind == "reference" else "oracle/fec_oracle.c restatement")}
+
+
+def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
+    """bench/bench_zfec.py:78-117 semantics: 10^6 random bytes split into k
+    blocks (last one zero-padded), `reps` encodes of all m blocks, then
+    primary-only and secondary-only (blocks k..2k-1) decodes; results in the
+    reference's units ("MB/s": encode = input bytes / 2^20 / s, decode = all m
+    blocks' bytes / 2^20 / s, README.rst:118-127)."""
+    d = os.urandom(size)
+    bs = -(-size // k)
+    ds = [d[i * bs:(i + 1) * bs] for i in range(k)]
+    ds[-1] = ds[-1] + b"\x00" * (len(ds[-2]) - len(ds[-1]))
+    enc = Encoder(k, m)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc.encode(ds)
+    enc_s = (time.perf_counter() - t0) / reps
+    blocks = enc.encode(ds)
+    nums = list(range(len(blocks)))
+    dec = Decoder(k, m)
+    res = {"encode_MBps": size / 2 ** 20 / enc_s}
+    for name, sl in (("decode_primary_MBps", slice(0, k)), ("decode_secondary_MBps", slice(k, 2 * k))):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dec.decode(blocks[sl], nums[sl])
+        el = (time.perf_counter() - t0) / reps
+        assert b"".join(dec.decode(blocks[sl], nums[sl]))[:size] == d
+        res[name] = sum(len(b) for b in blocks) / 2 ** 20 / el
+    return {key: round(v, 1) for key, v in res.items()}
 
 
 def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
@@ -364,6 +394,21 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, k, m, csz)
         except Exception as e:  # the baseline must never sink the GPU measurement
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if not args.no_extra and args.workload == "cfg2":
+            # configs[0]: the reference's own harness (bench/bench_zfec.py), 1 thread, on the
+            # reference C module, next to the same harness on this engine's bytes API
+            try:
+                from oracle import oracle
+
+                ref = oracle.ref_module()
+                bz = {"harness": "bench/bench_zfec.py semantics, K=3 M=10, 10^6 B, 1000 reps, 1 thread, "
+                                 "reference units (MB/s = 2^20 B/s)"}
+                if ref is not None:
+                    bz["cpu_reference"] = bench_zfec_style(ref.Encoder, ref.Decoder)
+                bz["gpu_bytes_api"] = bench_zfec_style(zfec_amd.Encoder, zfec_amd.Decoder)
+                out["cpu_baseline"]["bench_zfec"] = bz
+            except Exception as e:
+                out["cpu_baseline"]["bench_zfec"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
