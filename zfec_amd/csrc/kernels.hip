@@ -431,7 +431,9 @@ __host__ __device__ constexpr uint32_t table_rows(uint32_t r, uint32_t rt) {
     return MODE == kTilesPadded ? (r + rt - 1) / rt * rt : r;
 }
 
-template <bool ACC, bool NT, int RT_, int D, int GG, int MODE>
+// PROBE (microbenchmarks only, tools/mb_encode.hip): 1 = no memory traffic
+// (inputs synthesised, outputs dropped), 2 = no arithmetic (XOR of inputs).
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE, int PROBE = 0>
 __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     constexpr uint32_t CH = 4 * D;
     extern __shared__ LdsTab lds_tab[];
@@ -451,7 +453,14 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
         const uint64_t ib = st.u.s * job.in_sstride + sp.off;
 #pragma unroll
         for (int jj = 0; jj < GG; ++jj)
-            if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
+            if (st.g + jj < k) {
+                if constexpr (PROBE == 1) {
+#pragma unroll
+                    for (int v = 0; v < D; ++v) x[jj].w[v] = static_cast<uint32_t>(ib) * 0x9E3779B9u + st.g + jj + v;
+                } else {
+                    x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
+                }
+            }
     };
     Step cur{UnitIter(job), 0u, 0u};
     bool live = cur.u.s < job.nstripes;
@@ -486,7 +495,14 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
         Words<D> xb[GG];
         if (nlive) load_step(nxt, xb);
         if (live) {
-            mac_group<MODE == kTilesPadded, RT_, D, GG>(a, xa, lds_tab, cur.g, cur.rb, k, rp);
+            if constexpr (PROBE == 2) {
+#pragma unroll
+                for (int jj = 0; jj < GG; ++jj)
+#pragma unroll
+                    for (int v = 0; v < D; ++v) a[jj % RT_][v] ^= xa[jj].w[v];
+            } else {
+                mac_group<MODE == kTilesPadded, RT_, D, GG>(a, xa, lds_tab, cur.g, cur.rb, k, rp);
+            }
             if (tile_end) {
                 const Span sp = chunk_span<CH, !ACC>(cur.u.c, sz, nfull);
                 const uint64_t ob = cur.u.s * job.out_sstride + sp.off;
@@ -502,7 +518,11 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
 #pragma unroll
                         for (int v = 0; v < D; ++v) y.w[v] ^= o.w[v];
                     }
-                    store_words<D, NT>(op, y, sp.full, sp.nb);
+                    if constexpr (PROBE == 1) {
+                        if (y.w[0] == 0x12345678u && y.w[D - 1] == 0x9abcdef0u) store_words<D, NT>(op, y, sp.full, sp.nb);
+                    } else {
+                        store_words<D, NT>(op, y, sp.full, sp.nb);
+                    }
                 }
             }
         }
@@ -519,9 +539,9 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     }
 }
 
-template <bool ACC, bool NT, int RT_, int D, int GG, int MODE = kTilesRagged>
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE = kTilesRagged, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
-    matapply_lds_body<ACC, NT, RT_, D, GG, MODE>(job);
+    matapply_lds_body<ACC, NT, RT_, D, GG, MODE, PROBE>(job);
 }
 
 // ---------------------------------------------------------------------------
