@@ -18,7 +18,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC 
 
 all: $(LIB) $(PYEXT) oracle
 
-$(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp
+$(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp $(SRC)/bitslice.hpp
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp include/zfec_hip.h
@@ -27,8 +30,8 @@ $(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp include
 $(SRC)/gf256.o: $(SRC)/gf256.cpp $(SRC)/gf256.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -lpthread
 
 $(PYEXT): $(SRC)/fecmodule.cpp include/zfec_hip.h $(LIB)
 	$(CXX) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(PYINC) -o $@ $< -Lzfec_amd -lzfec_hip -Wl,-rpath,'$$ORIGIN'

@@ -145,9 +145,33 @@ int fec_device_count(void);
 /* Library version string. */
 const char* fec_version(void);
 
-/* Name of the kernel variant a launch with k inputs and r outputs uses
- * (diagnostics and profiling; k <= 32, r <= 48 per launch). */
+/* Name of the table-kernel variant a launch with k inputs and r outputs uses
+ * when no run-time specialised kernel applies (diagnostics and profiling;
+ * k <= 32, r <= 48 per launch). */
 const char* fec_kernel_name(unsigned k, unsigned r);
+
+/* Name of the kernel the calling thread launched last. */
+const char* fec_last_kernel_name(void);
+
+/* Run-time specialised bit-sliced kernels (hipRTC; zfec_amd/csrc/bitslice.cpp):
+ * the coefficient matrix of a launch compiled into the instruction stream.
+ * mode 0 = off; 1 = auto (default; large launches of wide codes, compiled in a
+ * background thread while the table kernels serve, then cached in memory and
+ * in jit_cache/ next to the library); 2 = force (every launch with blocks of
+ * >= 2048 bytes, compiled synchronously).  The environment variable
+ * ZFEC_HIP_JIT=0|auto|force sets the initial mode.  Returns the previous
+ * mode; any other value of `mode` only queries.  Results are bit-identical in
+ * every mode. */
+int fec_jit_mode(int mode);
+
+/* Wait for background compiles; returns the number of compiled kernels. */
+int fec_jit_wait(void);
+
+/* Compile now (no GPU needed) the kernels an fec_encode of block_nums, or an
+ * fec_decode from `index` (flags as fec_decode_ex), would use.  FEC_OK, or
+ * FEC_EHIP with the compiler's message. */
+int fec_jit_prepare_encode(const fec_t* code, const unsigned* block_nums, size_t num_block_nums);
+int fec_jit_prepare_decode(const fec_t* code, const unsigned* index, unsigned flags);
 
 #ifdef __cplusplus
 }

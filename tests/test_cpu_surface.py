@@ -182,6 +182,24 @@ def test_decode_rejects_what_reference_mishandles():
         e.encode([b"a", b"bb", b"c"])
 
 
+def test_jit_prepare_compiles_without_gpu(tmp_path, monkeypatch):
+    """fec_jit_prepare_encode / _decode generate and compile (hipRTC, gfx950)
+    the bit-sliced kernels a K=10/M=16 encode and a decode from blocks 6..15
+    would launch, and cache the code objects; no GPU involved."""
+    monkeypatch.setenv("ZFEC_HIP_JIT_CACHE", str(tmp_path))
+    code = capi.Code(10, 16)
+    code.jit_prepare_encode(list(range(10, 16)))
+    code.jit_prepare_decode([10, 11, 12, 13, 14, 15, 6, 7, 8, 9])
+    files = sorted(tmp_path.glob("zfec_hip_bitslice_k10_r*.co"))
+    assert len(files) == 2, files
+    for f in files:
+        assert f.read_bytes()[:4] == b"\x7fELF"
+    code.jit_prepare_encode(list(range(10, 16)))  # in-memory hit: nothing new
+    assert len(list(tmp_path.glob("*.co"))) == 2
+    with pytest.raises(capi.FecError):
+        code.jit_prepare_decode([0, 0, 1, 2, 3, 4, 5, 6, 7, 8])  # duplicate: rejected before compiling
+
+
 @pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")
 def test_no_gpu_fails_loudly():
     with pytest.raises(zfec_amd.Error, match="no GPU"):

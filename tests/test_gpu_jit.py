@@ -1,0 +1,161 @@
+"""GPU parity of the run-time specialised bit-sliced kernels
+(zfec_amd/csrc/bitslice.cpp): bit-exact against the CPU oracle across code
+shapes, block sizes around the 2 KiB unit and its overlapping last chunk,
+batched strided stripes at misaligned bases (with guard bytes that must stay
+untouched), and the auto policy (background compile; the table kernels serve
+until it is ready, with identical results)."""
+import numpy as np
+import pytest
+
+import zfec_amd
+from zfec_amd import capi
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if zfec_amd.device_count() < 1:
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+
+
+@pytest.fixture
+def force_jit():
+    prev = capi.jit_mode(capi.JIT_FORCE)
+    yield
+    capi.jit_mode(prev)
+
+
+def place(nums, k):
+    """slot order with primary i at slot i (zfec/_fecmodule.c:482-493)."""
+    slots = [None] * k
+    sec = iter([n for n in nums if n >= k])
+    for n in nums:
+        if n < k:
+            slots[n] = n
+    return [s if s is not None else next(sec) for s in slots]
+
+
+# (k, m): few/many inputs and outputs, one and several register tiles
+JIT_SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40)]
+
+
+@pytest.mark.parametrize("k,m", JIT_SHAPES)
+def test_jit_encode_decode_vs_oracle(force_jit, k, m):
+    rng = np.random.default_rng(k * 100 + m)
+    for sz in [2048, 2049, 3000, 4096, 65536 + 17]:
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        assert capi.last_kernel_name().startswith("zfec_hip_bitslice"), capi.last_kernel_name()
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        nums = list(range(m - k, m))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        if any(n >= k for n in nums):
+            assert capi.last_kernel_name().startswith("zfec_hip_bitslice"), capi.last_kernel_name()
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz)
+
+
+@pytest.mark.parametrize("k,m,sz,ns", [(10, 16, 5000, 7), (20, 60, 52429, 3), (4, 12, 2048, 33)])
+def test_jit_batched_strided_misaligned(force_jit, k, m, sz, ns):
+    """Stripes at an odd row stride from odd base offsets; the gaps between rows
+    and the bytes around the buffers must stay zero (the overlapping last chunk
+    writes only inside [0, sz) of each row)."""
+    r = m - k
+    ld = sz + 13
+    rng = np.random.default_rng(sz + ns)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    host = np.zeros(5 + ns * k * ld + 64, dtype=np.uint8)
+    rows = host[5:5 + ns * k * ld].reshape(ns, k, ld)
+    rows[:, :, :sz] = data
+    src = torch.from_numpy(host).cuda()
+    dst = torch.zeros(3 + ns * r * ld + 64, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(src.data_ptr() + 5, ld, k * ld, dst.data_ptr() + 3, ld, r * ld, list(range(k, m)), sz, ns,
+                      stream=st)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name().startswith("zfec_hip_bitslice")
+    got = dst.cpu().numpy()
+    assert got[:3].sum() == 0 and got[3 + ns * r * ld:].sum() == 0
+    out = got[3:3 + ns * r * ld].reshape(ns, r, ld)
+    assert out[:, :, sz:].sum() == 0
+    for s in range(ns):
+        assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s
+    # decode every stripe from its last k blocks, same strided layout
+    slots = place(list(range(m - k, m)), k)
+    allb = np.concatenate([data, out[:, :, :sz]], axis=1)
+    recv_host = np.zeros(7 + ns * k * ld, dtype=np.uint8)
+    recv_host[7:].reshape(ns, k, ld)[:, :, :sz] = allb[:, slots, :]
+    recv = torch.from_numpy(recv_host).cuda()
+    missing = [i for i in range(k) if slots[i] >= k]
+    rec = torch.zeros(1 + ns * len(missing) * ld + 64, dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr() + 7, ld, k * ld, rec.data_ptr() + 1, ld, len(missing) * ld, slots, sz, ns,
+                      stream=st)
+    torch.cuda.synchronize()
+    rg = rec.cpu().numpy()
+    assert rg[0] == 0 and rg[1 + ns * len(missing) * ld:].sum() == 0
+    rv = rg[1:1 + ns * len(missing) * ld].reshape(ns, len(missing), ld)
+    assert (rv[:, :, :sz] == data[:, missing, :]).all()
+    assert rv[:, :, sz:].sum() == 0
+
+
+def test_jit_all_primaries_flag(force_jit):
+    """FEC_FLAG_ALL_PRIMARIES through the specialised kernel: identity rows copy."""
+    k, m, sz, ns = 6, 14, 4100, 5
+    nums = [7, 1, 9, 3, 12, 13]
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    allb = np.concatenate([data, np.stack([oracle.encode(k, m, data[s]) for s in range(ns)])], axis=1)
+    slots = place(nums, k)
+    recv = torch.from_numpy(np.ascontiguousarray(allb[:, slots, :])).cuda()
+    out = torch.zeros((ns, k, sz), dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr(), sz, k * sz, out.data_ptr(), sz, k * sz, slots, sz, ns,
+                      stream=torch.cuda.current_stream().cuda_stream,
+                      flags=capi.FEC_FLAG_ASYNC | capi.FEC_FLAG_ALL_PRIMARIES)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name().startswith("zfec_hip_bitslice")
+    assert (out.cpu().numpy() == data).all()
+
+
+def test_jit_auto_policy_background_compile():
+    """Auto mode: the first large launch queues a compile and runs the table
+    kernel; after fec_jit_wait the specialised kernel runs; same bytes."""
+    prev = capi.jit_mode(capi.JIT_AUTO)
+    try:
+        k, m, sz = 12, 21, 4 << 20  # (k + r) * sz = 84 MiB per launch: above the auto threshold
+        g = torch.Generator(device="cuda").manual_seed(12)
+        data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda", generator=g)
+        enc = zfec_amd.Encoder(k, m)
+        out1 = enc.encode([data[i] for i in range(k)])
+        first = capi.last_kernel_name()
+        capi.jit_wait()
+        out2 = enc.encode([data[i] for i in range(k)])
+        second = capi.last_kernel_name()
+        assert first.startswith("matapply"), first
+        assert second.startswith("zfec_hip_bitslice"), (first, second)
+        for a, b in zip(out1[k:], out2[k:]):
+            assert bool(torch.equal(a, b))
+        lo, hi = sz // 3, sz // 3 + 50000
+        par = torch.stack(out2[k:])[:, lo:hi].cpu().numpy()
+        assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all()
+    finally:
+        capi.jit_mode(prev)
+
+
+def test_jit_off_uses_table_kernels():
+    prev = capi.jit_mode(capi.JIT_OFF)
+    try:
+        k, m, sz = 20, 60, 52429
+        data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda")
+        out = zfec_amd.Encoder(k, m).encode([data[i] for i in range(k)])
+        assert capi.last_kernel_name().startswith("matapply"), capi.last_kernel_name()
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data.cpu().numpy())).all()
+    finally:
+        capi.jit_mode(prev)

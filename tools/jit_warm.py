@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Compile (hipRTC, no GPU needed) the bit-sliced kernels the GPU tests and the
+bench workloads launch, into zfec_amd/jit_cache/ next to libzfec_hip.so, so a
+fresh GPU box loads them instead of compiling.  The ZFEC_HIP_JIT_* knobs in the
+environment select the variant (tools/jit_bench.py sets them per variant)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from zfec_amd import capi  # noqa: E402
+
+
+def place(nums, k):
+    slots = [None] * k
+    sec = iter([n for n in nums if n >= k])
+    for n in nums:
+        if n < k:
+            slots[n] = n
+    return [s if s is not None else next(sec) for s in slots]
+
+
+# (k, m): tests/test_gpu_jit.py shapes, the auto-policy shape, bench cfg3 / cfg4
+SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (4, 12), (12, 21)]
+
+
+def main():
+    t0 = time.time()
+    for k, m in SHAPES:
+        code = capi.Code(k, m)
+        code.jit_prepare_encode(list(range(k, m)))
+        code.jit_prepare_decode(place(list(range(m - k, m)), k))
+    code = capi.Code(6, 14)
+    code.jit_prepare_decode(place([7, 1, 9, 3, 12, 13], 6), capi.FEC_FLAG_ALL_PRIMARIES)
+    print("jit_warm: %d kernels ready in %.1f s" % (capi.jit_wait(), time.time() - t0))
+
+
+if __name__ == "__main__":
+    main()

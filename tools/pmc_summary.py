@@ -9,11 +9,13 @@ Reads gpurun_out/<tag>/<workload>/{ktrace,fetch,write}/*.csv (rocprofv3
   profiles/pmc_summary.json     {"encode_<workload>": ..., "decode_<workload>": ...}
                                 (read by bench.py for roofline.traffic)
 
-Roles come from dispatch order, which bench.py fixes (run_workload): one
-encode, then (encode, decode) pairs: warmup + 3 + steps + 50 timed by
-per-launch events.  Encode and decode of one workload can be the
-same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes 6), so
-names alone do not tell them apart.
+Roles come from dispatch order, which bench.py fixes (run_workload):
+(encode, decode) pairs from the first launch on: staging pair, warmup, 3,
+steps, 50 timed by per-launch events.  Encode and decode of one workload can
+be the same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes
+6), so names alone do not tell them apart.  Per role only the launches of its
+most frequent kernel count: the first launches of a wide code run the table
+kernel while its bit-sliced kernel compiles (zfec_amd/csrc/bitslice.cpp).
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE (KiB) reads exactly half
 of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is
@@ -30,7 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     name = name.replace("void zfec_hip::(anonymous namespace)::", "")
-    return name.split("(zfec_hip::MatJob)")[0][:80]
+    return name.split("(zfec_hip::MatJob)")[0].split("(Args)")[0][:80]
 
 
 def load(path):
@@ -39,7 +41,7 @@ def load(path):
 
 
 def roles(n):
-    return ["encode" if i == 0 or (i - 1) % 2 == 0 else "decode" for i in range(n)]
+    return ["encode" if i % 2 == 0 else "decode" for i in range(n)]
 
 
 def ours(rows):
@@ -61,13 +63,21 @@ def summarize(src):
     res = {}
     for rows, col in ((kt, "dur_ns"), (fe, "fetch_kib"), (wr, "write_kib")):
         for r, role in zip(rows, roles(len(rows))):
-            e = res.setdefault(role, {"kernel": short(r["Kernel_Name"]), "dur_ns": [], "fetch_kib": [], "write_kib": []})
+            e = res.setdefault(role, {"kernel": "", "names": [], "dur_ns": [], "fetch_kib": [], "write_kib": [],
+                                      "names_dur_ns": [], "names_fetch_kib": [], "names_write_kib": []})
+            e["names_" + col].append(r["Kernel_Name"])
             if col == "dur_ns":
+                e["names"].append(r["Kernel_Name"])
                 e[col].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             else:
                 e[col].append(float(r["Counter_Value"]))
     out = {}
     for role, e in res.items():
+        names = e.pop("names")
+        main = max(set(names), key=names.count)
+        for col in ("dur_ns", "fetch_kib", "write_kib"):
+            e[col] = [v for v, nm in zip(e[col], e["names_" + col]) if nm == main]
+        e["kernel"] = short(main)
         mean = lambda v: sum(v) / len(v) if v else None
         fetch, write = mean(e["fetch_kib"]), mean(e["write_kib"])
         out[role] = {"kernel": e["kernel"], "launches": len(e["dur_ns"]),

@@ -40,7 +40,14 @@ SYMBOLS = [
     ("fec_device_count", ctypes.c_int, []),
     ("fec_version", ctypes.c_char_p, []),
     ("fec_kernel_name", ctypes.c_char_p, [_U, _U]),
+    ("fec_last_kernel_name", ctypes.c_char_p, []),
+    ("fec_jit_mode", ctypes.c_int, [ctypes.c_int]),
+    ("fec_jit_wait", ctypes.c_int, []),
+    ("fec_jit_prepare_encode", ctypes.c_int, [_P, _UP, _SZ]),
+    ("fec_jit_prepare_decode", ctypes.c_int, [_P, _UP, _U]),
 ]
+
+JIT_OFF, JIT_AUTO, JIT_FORCE = 0, 1, 2
 
 
 class FecT(ctypes.Structure):
@@ -85,6 +92,21 @@ def variant_name(k, r):
     return lib().fec_kernel_name(k, r).decode()
 
 
+def last_kernel_name():
+    """Kernel the calling thread launched last (fec_last_kernel_name)."""
+    return lib().fec_last_kernel_name().decode()
+
+
+def jit_mode(mode=-1):
+    """Set the bit-sliced JIT mode (JIT_OFF / JIT_AUTO / JIT_FORCE); returns the previous one."""
+    return lib().fec_jit_mode(mode)
+
+
+def jit_wait():
+    """Wait for background JIT compiles; number of compiled kernels."""
+    return lib().fec_jit_wait()
+
+
 def ptr_array(addrs):
     return (ctypes.c_void_p * max(1, len(addrs)))(*addrs)
 
@@ -110,6 +132,12 @@ class Code(object):
     def enc_matrix(self):
         s = ctypes.cast(self.ptr, ctypes.POINTER(FecT)).contents
         return bytes(s.enc_matrix[: self.k * self.m])
+
+    def jit_prepare_encode(self, block_nums):
+        check(lib().fec_jit_prepare_encode(self.ptr, uint_array(block_nums), len(block_nums)))
+
+    def jit_prepare_decode(self, index, flags=0):
+        check(lib().fec_jit_prepare_decode(self.ptr, uint_array(index), flags))
 
     def encode_batch(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
         check(lib().fec_encode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(block_nums),

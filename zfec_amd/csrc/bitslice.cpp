@@ -1,0 +1,582 @@
+// bitslice.cpp -- source generator and hipRTC JIT cache of the bit-sliced
+// GF(2^8) matrix-apply kernels (see bitslice.hpp).
+//
+// The kernel computes the same thing as matapply_* in kernels.hip -- for each
+// stripe, out_i = sum_j C[i][j] * in_j over GF(2^8), the work of fec_encode
+// (zfec/fec.c:487-505) and fec_decode (zfec/fec.c:527-557) -- with the
+// coefficient matrix compiled into the instruction stream.
+//
+// Per wave and unit: 2 KiB of each block (lane l owns bytes 16l..16l+15 and
+// 1024+16l..1024+16l+15, so every load and store instruction is 1 KiB
+// contiguous).  The 32 bytes of a lane are transposed into 8 bit-planes
+// (plane a = bit a of all 32 bytes); an output plane b of c*x is the XOR of the
+// input planes a with bit b of c*2^a set.  Rows are processed in register
+// tiles of up to kBsMaxTile outputs (8 accumulator planes each); inside a tile
+// every input is loaded, transposed, expanded into the XOR combinations of its
+// planes 0-3 (L[1..15]) and 4-7 (H[1..15]), and each accumulator plane takes
+// one XOR3 (acc ^ L[lo] ^ H[hi]).  The accumulators are transposed back to
+// bytes and stored with streaming stores.
+#include "bitslice.hpp"
+
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include <hip/hiprtc.h>
+
+#include "gf256.hpp"
+
+namespace zfec_hip {
+namespace {
+
+// masks[b]: bit a is set iff bit b of c*x depends on bit a of x, i.e. iff bit
+// b of c * 2^a (2 = alpha, zfec/fec.c:16) is set.
+void coef_masks(uint8_t c, uint8_t masks[8]) {
+    const Field& f = field();
+    for (int b = 0; b < 8; ++b) {
+        unsigned m = 0;
+        for (int a = 0; a < 8; ++a)
+            if ((f.mul[c][1u << a] >> b) & 1u) m |= 1u << a;
+        masks[b] = static_cast<uint8_t>(m);
+    }
+}
+
+struct Src {
+    std::string s;
+    void operator()(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        const int n = vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        if (n > 0) s.append(buf, static_cast<size_t>(n) < sizeof buf ? static_cast<size_t>(n) : sizeof buf - 1);
+    }
+};
+
+const char* const kPrelude = R"(typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef unsigned char u8;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+// v_bitop3_b32 truth tables index the operands as S0 = 0xF0, S1 = 0xCC, S2 = 0xAA
+__device__ __forceinline__ u32 x3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+__device__ __forceinline__ u32 sel(u32 m, u32 a, u32 b) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0xE4); }  // m ? a : b
+// one block swap of an 8x8 bit-matrix transpose, four byte lanes at once:
+// a <- (a & m) | ((b << s) & ~m),  b <- ((a >> s) & m) | (b & ~m)
+__device__ __forceinline__ void sw(u32& a, u32& b, int s, u32 m) {
+    const u32 t0 = sel(m, a, b << s);
+    const u32 t1 = sel(m, a >> s, b);
+    a = t0;
+    b = t1;
+}
+// 8 dwords (32 bytes) <-> 8 bit-planes; the transpose is its own inverse
+__device__ __forceinline__ void tr8(u32& v0, u32& v1, u32& v2, u32& v3, u32& v4, u32& v5, u32& v6, u32& v7) {
+    sw(v0, v4, 4, 0x0F0F0F0Fu); sw(v1, v5, 4, 0x0F0F0F0Fu); sw(v2, v6, 4, 0x0F0F0F0Fu); sw(v3, v7, 4, 0x0F0F0F0Fu);
+    sw(v0, v2, 2, 0x33333333u); sw(v1, v3, 2, 0x33333333u); sw(v4, v6, 2, 0x33333333u); sw(v5, v7, 2, 0x33333333u);
+    sw(v0, v1, 1, 0x55555555u); sw(v2, v3, 1, 0x55555555u); sw(v4, v5, 1, 0x55555555u); sw(v6, v7, 1, 0x55555555u);
+}
+// Buffer loads / stores off a wave-uniform base (block pointer + the unit's
+// offset, in SGPRs) with the lane's 32-bit offset: no 64-bit VGPR address per
+// block.  aux 2 = nt (streaming store).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const u8* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(p), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ld(__amdgpu_buffer_rsrc_t r, u32 off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, u32 off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 2);
+}
+)";
+
+// Name of the XOR of input planes {base + a : bit a of m} of step n (m != 0),
+// emitting the combinations it needs on first use.
+struct Combos {
+    unsigned n;
+    char side;      // 'L' (planes 0-3) or 'H' (planes 4-7)
+    unsigned base;  // 0 or 4
+    bool have[16] = {};
+    std::string name(unsigned m, Src& e) {
+        char b[32];
+        if ((m & (m - 1)) == 0) {  // one plane
+            snprintf(b, sizeof b, "q%u_%u", n, base + static_cast<unsigned>(__builtin_ctz(m)));
+            return b;
+        }
+        snprintf(b, sizeof b, "%c%u_%u", side, n, m);
+        if (!have[m]) {
+            const unsigned top = 1u << (31 - __builtin_clz(m));
+            const std::string rest = name(m ^ top, e), one = name(top, e);
+            e("    const u32 %s = %s ^ %s;\n", b, rest.c_str(), one.c_str());
+            have[m] = true;
+        }
+        return b;
+    }
+};
+
+}  // namespace
+
+std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name) {
+    field_init();
+    const unsigned maxt = opt.max_tile ? opt.max_tile : kBsMaxTile;
+    const unsigned ntiles = (r + maxt - 1) / maxt;
+    std::vector<unsigned> tile_lo(ntiles + 1);
+    for (unsigned t = 0; t <= ntiles; ++t) tile_lo[t] = t * r / ntiles;  // near-equal tiles
+    std::vector<uint8_t> masks(size_t(r) * k * 8);
+    for (unsigned i = 0; i < r; ++i)
+        for (unsigned j = 0; j < k; ++j) coef_masks(coef[i * k + j], &masks[(size_t(i) * k + j) * 8]);
+
+    Src e;
+    e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
+    e.s += kPrelude;
+    e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
+    e("extern \"C\" __global__ __launch_bounds__(256) void %s(const Args a) {\n", name);
+    e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n");
+    e("  const u32 wid = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
+    e("  u32 s = wid / a.cps, c = wid - s * a.cps;\n");
+    e("  while (s < a.nstripes) {\n");
+    e("    u64 off = (u64)c * %uu;\n", kBsChunk);
+    e("    if (off > a.sz - %uu) off = a.sz - %uu;  // the last chunk ends at sz (overlapping its neighbour)\n",
+      kBsChunk, kBsChunk);
+    e("    const u64 ub = (u64)s * a.iss + off, uo = (u64)s * a.oss + off;\n");
+
+    // Steps: (tile t, input j) in order; loads run `prefetch` steps ahead.
+    const unsigned nsteps = ntiles * k;
+    const unsigned pf = opt.prefetch;
+    auto emit_load = [&](unsigned n) {
+        const unsigned j = n % k;
+        e("    const __amdgpu_buffer_rsrc_t ri%u = rs(a.in[%u] + ub);\n", n, j);
+        e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", n, n, n, n);
+    };
+    for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
+    for (unsigned t = 0; t < ntiles; ++t) {
+        const unsigned r0 = tile_lo[t], r1 = tile_lo[t + 1];
+        e("    // tile %u: rows %u..%u\n", t, r0, r1 - 1);
+        std::vector<char> init(size_t(r1 - r0) * 8, 0);
+        for (unsigned i = r0; i < r1; ++i)
+            e("    u32 a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7;\n", i, i, i, i, i, i, i, i);
+        for (unsigned j = 0; j < k; ++j) {
+            const unsigned n = t * k + j;
+            if (pf == 0)
+                emit_load(n);
+            else if (n + pf < nsteps)
+                emit_load(n + pf);
+            e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", n, n, n, n, n, n, n, n);
+            e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", n, n, n, n, n, n, n, n);
+            e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
+            Combos lo{n, 'L', 0}, hi{n, 'H', 4};
+            for (unsigned i = r0; i < r1; ++i) {
+                const uint8_t* mk = &masks[(size_t(i) * k + j) * 8];
+                for (unsigned b = 0; b < 8; ++b) {
+                    const unsigned m = mk[b];
+                    if (!m) continue;
+                    char acc[32];
+                    snprintf(acc, sizeof acc, "a%u_%u", i, b);
+                    char& ini = init[size_t(i - r0) * 8 + b];
+                    const unsigned ml = m & 15u, mh = m >> 4;
+                    const std::string sl = ml ? lo.name(ml, e) : std::string();
+                    const std::string sh = mh ? hi.name(mh, e) : std::string();
+                    if (!ini) {
+                        if (ml && mh)
+                            e("    %s = %s ^ %s;\n", acc, sl.c_str(), sh.c_str());
+                        else
+                            e("    %s = %s;\n", acc, ml ? sl.c_str() : sh.c_str());
+                        ini = 1;
+                    } else if (ml && mh) {
+                        e("    %s = x3(%s, %s, %s);\n", acc, acc, sl.c_str(), sh.c_str());
+                    } else {
+                        e("    %s ^= %s;\n", acc, ml ? sl.c_str() : sh.c_str());
+                    }
+                }
+            }
+            if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
+        }
+        for (unsigned i = r0; i < r1; ++i) {
+            for (unsigned b = 0; b < 8; ++b)
+                if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
+            e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
+            e("    const __amdgpu_buffer_rsrc_t ro%u = rs(a.out[%u] + uo);\n", i, i);
+            e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
+            e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
+        }
+    }
+    e("    c += a.gs_c;\n    s += a.gs_s;\n    if (c >= a.cps) { c -= a.cps; ++s; }\n  }\n}\n");
+    return e.s;
+}
+
+// ============================================================================
+// hipRTC, disk cache, registry
+// ============================================================================
+namespace {
+
+typedef hiprtcResult (*CreateFn)(hiprtcProgram*, const char*, const char*, int, const char**, const char**);
+typedef hiprtcResult (*CompileFn)(hiprtcProgram, int, const char**);
+typedef hiprtcResult (*SizeFn)(hiprtcProgram, size_t*);
+typedef hiprtcResult (*GetFn)(hiprtcProgram, char*);
+typedef hiprtcResult (*DestroyFn)(hiprtcProgram*);
+
+struct Rtc {
+    bool ok = false;
+    std::string err;
+    CreateFn create = nullptr;
+    CompileFn compile = nullptr;
+    SizeFn log_size = nullptr, code_size = nullptr;
+    GetFn log = nullptr, code = nullptr;
+    DestroyFn destroy = nullptr;
+};
+
+const Rtc& rtc() {
+    static const Rtc r = [] {
+        Rtc x;
+        void* h = nullptr;
+        for (const char* n : {"libhiprtc.so.7", "libhiprtc.so", "/opt/rocm/lib/libhiprtc.so.7", "/opt/rocm/lib/libhiprtc.so"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            const char* d = dlerror();
+            x.err = std::string("hipRTC not loadable: ") + (d ? d : "?");
+            return x;
+        }
+        x.create = reinterpret_cast<CreateFn>(dlsym(h, "hiprtcCreateProgram"));
+        x.compile = reinterpret_cast<CompileFn>(dlsym(h, "hiprtcCompileProgram"));
+        x.log_size = reinterpret_cast<SizeFn>(dlsym(h, "hiprtcGetProgramLogSize"));
+        x.log = reinterpret_cast<GetFn>(dlsym(h, "hiprtcGetProgramLog"));
+        x.code_size = reinterpret_cast<SizeFn>(dlsym(h, "hiprtcGetCodeSize"));
+        x.code = reinterpret_cast<GetFn>(dlsym(h, "hiprtcGetCode"));
+        x.destroy = reinterpret_cast<DestroyFn>(dlsym(h, "hiprtcDestroyProgram"));
+        x.ok = x.create && x.compile && x.log_size && x.log && x.code_size && x.code && x.destroy;
+        if (!x.ok) x.err = "hipRTC symbols missing";
+        return x;
+    }();
+    return r;
+}
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+    for (unsigned char ch : s) {
+        h ^= ch;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+const char* const kRtcOptions[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-mcode-object-version=5"};
+constexpr int kRtcNumOptions = sizeof(kRtcOptions) / sizeof(kRtcOptions[0]);
+
+// Directory of the code-object cache: $ZFEC_HIP_JIT_CACHE ("" disables it),
+// else jit_cache/ next to libzfec_hip.so (in-tree: compiled kernels travel
+// with the build), if writable.
+std::string cache_dir() {
+    if (const char* e = getenv("ZFEC_HIP_JIT_CACHE")) return e;
+    Dl_info info;
+    if (!dladdr(reinterpret_cast<void*>(&cache_dir), &info) || !info.dli_fname) return std::string();
+    std::string lib = info.dli_fname;
+    const size_t slash = lib.rfind('/');
+    const std::string d = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/jit_cache";
+    mkdir(d.c_str(), 0755);
+    return access(d.c_str(), W_OK | X_OK) == 0 ? d : std::string();
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::vector<char> buf;
+    char tmp[65536];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+    fclose(f);
+    if (buf.size() < 64 || memcmp(buf.data(), "\x7f" "ELF", 4) != 0) return false;
+    out.swap(buf);
+    return true;
+}
+
+void write_file_atomic(const std::string& path, const std::vector<char>& data) {
+    char suffix[64];
+    snprintf(suffix, sizeof suffix, ".tmp.%d.%zx", static_cast<int>(getpid()),
+             std::hash<std::thread::id>()(std::this_thread::get_id()));
+    const std::string tmp = path + suffix;
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+    if (fclose(f) == 0 && ok && rename(tmp.c_str(), path.c_str()) == 0) return;
+    unlink(tmp.c_str());
+}
+
+// Code object for `src`: the disk cache, else hipRTC.
+bool compile_code(const std::string& src, const std::string& name, std::vector<char>& code, std::string& err) {
+    std::string opts;
+    for (const char* o : kRtcOptions) (opts += o) += ' ';
+    char hex[32];
+    snprintf(hex, sizeof hex, "%016llx", static_cast<unsigned long long>(fnv1a(src, fnv1a(opts))));
+    const std::string dir = cache_dir();
+    const std::string path = dir.empty() ? std::string() : dir + "/" + name + "-" + hex + ".co";
+    if (!path.empty() && read_file(path, code)) return true;
+    const Rtc& R = rtc();
+    if (!R.ok) {
+        err = R.err;
+        return false;
+    }
+    hiprtcProgram prog;
+    if (R.create(&prog, src.c_str(), (name + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        err = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const char* opt_list[kRtcNumOptions];
+    for (int i = 0; i < kRtcNumOptions; ++i) opt_list[i] = kRtcOptions[i];
+    const hiprtcResult cr = R.compile(prog, kRtcNumOptions, opt_list);
+    size_t n = 0;
+    if (cr != HIPRTC_SUCCESS) {
+        std::string log;
+        if (R.log_size(prog, &n) == HIPRTC_SUCCESS && n > 1) {
+            log.resize(n);
+            R.log(prog, &log[0]);
+        }
+        err = "hipRTC compile of " + name + " failed: " + log.substr(0, 2000);
+        R.destroy(&prog);
+        return false;
+    }
+    if (R.code_size(prog, &n) != HIPRTC_SUCCESS || n == 0) {
+        err = "hiprtcGetCodeSize failed";
+        R.destroy(&prog);
+        return false;
+    }
+    code.resize(n);
+    R.code(prog, code.data());
+    R.destroy(&prog);
+    if (!path.empty()) write_file_atomic(path, code);
+    return true;
+}
+
+struct Loaded {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    int blocks_per_cu = 1;
+    int num_cu = 256;
+};
+
+struct Entry {
+    int state = 0;  // 0 compiling, 1 ready, 2 failed
+    std::string name;
+    std::vector<char> code;
+    std::map<int, Loaded> dev;
+};
+
+struct Registry {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::string, std::unique_ptr<Entry>> entries;
+    int pending = 0, ready = 0;
+    std::vector<std::thread> workers;
+    std::string last_error;
+    bool atexit_set = false;
+};
+
+Registry& reg() {
+    static Registry* r = new Registry;  // never destroyed: compile threads may still run at exit
+    return *r;
+}
+
+void join_workers() {
+    Registry& R = reg();
+    std::vector<std::thread> w;
+    {
+        std::lock_guard<std::mutex> g(R.mu);
+        w.swap(R.workers);
+    }
+    for (auto& t : w)
+        if (t.joinable()) t.join();
+}
+
+void run_compile(Entry* e, std::string src) {
+    std::vector<char> code;
+    std::string err;
+    const bool ok = compile_code(src, e->name, code, err);
+    Registry& R = reg();
+    std::lock_guard<std::mutex> g(R.mu);
+    if (ok) {
+        e->code.swap(code);
+        e->state = 1;
+        ++R.ready;
+    } else {
+        e->state = 2;
+        R.last_error = err;
+        if (getenv("ZFEC_HIP_JIT_VERBOSE")) fprintf(stderr, "zfec_hip: %s\n", err.c_str());
+    }
+    --R.pending;
+    R.cv.notify_all();
+}
+
+std::atomic<int> g_mode{-1};
+
+unsigned env_uint(const char* name, unsigned dflt) {
+    const char* v = getenv(name);
+    return v && *v ? static_cast<unsigned>(strtoul(v, nullptr, 10)) : dflt;
+}
+
+BsOptions options_from_env() {
+    BsOptions o;
+    o.max_tile = env_uint("ZFEC_HIP_JIT_TILE", o.max_tile);
+    if (o.max_tile == 0 || o.max_tile > 32) o.max_tile = kBsMaxTile;
+    o.prefetch = env_uint("ZFEC_HIP_JIT_PREFETCH", o.prefetch);
+    if (o.prefetch > 4) o.prefetch = 4;
+    o.barriers = env_uint("ZFEC_HIP_JIT_BARRIER", 1) != 0;
+    return o;
+}
+
+// Registry entry for (matrix, options); queues or runs its compile.  Called
+// with R.mu held by `lk`; releases it while compiling synchronously.
+Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
+    Registry& R = reg();
+    const BsOptions opt = options_from_env();
+    std::string key;
+    key.reserve(32 + size_t(k) * r);
+    char hdr[64];
+    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0);
+    key += hdr;
+    key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
+    auto it = R.entries.find(key);
+    if (it != R.entries.end()) return it->second.get();
+    auto ne = std::make_unique<Entry>();
+    Entry* e = ne.get();
+    char nm[80];
+    snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
+    e->name = nm;
+    R.entries.emplace(key, std::move(ne));
+    ++R.pending;
+    std::string src = bitslice_source(coef, k, r, opt, nm);
+    if (sync) {
+        lk.unlock();
+        run_compile(e, std::move(src));
+        lk.lock();
+    } else {
+        if (!R.atexit_set) {
+            std::atexit(join_workers);
+            R.atexit_set = true;
+        }
+        R.workers.emplace_back(run_compile, e, std::move(src));
+    }
+    return e;
+}
+
+// The table kernels serve the rest: few coefficients (memory-bound), blocks
+// shorter than one unit, XOR-accumulating continuation passes, small launches
+// (auto mode).
+bool eligible(const MatJob& job, JitMode mode) {
+    if (mode == kJitOff || job.accumulate || job.tables || job.sz < static_cast<uint64_t>(kBsChunk) ||
+        job.nstripes == 0 || job.k == 0 || job.r == 0)
+        return false;
+    if (mode == kJitForce) return true;
+    if (job.k * job.r < 24 || (job.k <= 4 && job.r <= 8)) return false;
+    const double bytes = double(job.k + job.r) * double(job.sz) * double(job.nstripes);
+    return bytes >= double(32u << 20);
+}
+
+}  // namespace
+
+JitMode jit_mode() {
+    int m = g_mode.load();
+    if (m < 0) {
+        const char* e = getenv("ZFEC_HIP_JIT");
+        m = kJitAuto;
+        if (e && (!strcmp(e, "0") || !strcmp(e, "off"))) m = kJitOff;
+        if (e && (!strcmp(e, "2") || !strcmp(e, "force"))) m = kJitForce;
+        g_mode.store(m);
+    }
+    return static_cast<JitMode>(m);
+}
+
+void set_jit_mode(JitMode m) { g_mode.store(static_cast<int>(m)); }
+
+int jit_prepare(const uint8_t* coef, unsigned k, unsigned r) {
+    if (k == 0 || r == 0) return -1;
+    Registry& R = reg();
+    std::unique_lock<std::mutex> lk(R.mu);
+    Entry* e = get_entry(coef, k, r, true, lk);
+    R.cv.wait(lk, [&] { return e->state != 0; });
+    return e->state == 1 ? 0 : -1;
+}
+
+int jit_wait() {
+    Registry& R = reg();
+    std::unique_lock<std::mutex> lk(R.mu);
+    R.cv.wait(lk, [&] { return R.pending == 0; });
+    return R.ready;
+}
+
+std::string jit_last_error() {
+    Registry& R = reg();
+    std::lock_guard<std::mutex> g(R.mu);
+    return R.last_error;
+}
+
+hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char** name_out) {
+    const JitMode mode = jit_mode();
+    if (!eligible(job, mode)) return hipErrorNotSupported;
+    Registry& R = reg();
+    std::unique_lock<std::mutex> lk(R.mu);
+    Entry* e = get_entry(job.coef, job.k, job.r, mode == kJitForce, lk);
+    if (e->state == 0) {
+        if (mode != kJitForce) return hipErrorNotReady;
+        R.cv.wait(lk, [&] { return e->state != 0; });
+    }
+    if (e->state != 1) return hipErrorNotSupported;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
+    auto it = e->dev.find(dev);
+    if (it == e->dev.end()) {
+        Loaded L;
+        hipError_t er = hipModuleLoadData(&L.mod, e->code.data());
+        if (er == hipSuccess) er = hipModuleGetFunction(&L.fn, L.mod, e->name.c_str());
+        if (er != hipSuccess) {
+            (void)hipGetLastError();
+            e->state = 2;
+            R.last_error = std::string("loading ") + e->name + ": " + hipGetErrorString(er);
+            return hipErrorNotSupported;
+        }
+        int nb = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.fn, 256, 0) == hipSuccess && nb > 0)
+            L.blocks_per_cu = nb;
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+            L.num_cu = ncu;
+        it = e->dev.emplace(dev, L).first;
+    }
+    const Loaded L = it->second;
+    const char* name = e->name.c_str();  // stable: entries are never removed
+    lk.unlock();
+
+    const uint64_t cps = (job.sz + kBsChunk - 1) / kBsChunk;
+    const uint64_t waves = cps * job.nstripes;
+    if (waves >= (1ull << 32) - (1ull << 24)) return hipErrorNotSupported;
+    const uint64_t need = (waves + 3) / 4;
+    const uint64_t cap = uint64_t(L.num_cu) * L.blocks_per_cu * 64;
+    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+    const uint64_t gwaves = uint64_t(grid) * 4;
+    // struct Args of the generated source: 3 x u64, 4 x u32, k + r pointers
+    std::vector<uint64_t> args(5 + job.k + job.r);
+    args[0] = job.sz;
+    args[1] = job.in_sstride;
+    args[2] = job.out_sstride;
+    const uint32_t a32[4] = {job.nstripes, static_cast<uint32_t>(cps), static_cast<uint32_t>(gwaves % cps),
+                             static_cast<uint32_t>(gwaves / cps)};
+    std::memcpy(&args[3], a32, sizeof a32);
+    for (unsigned j = 0; j < job.k; ++j) args[5 + j] = reinterpret_cast<uint64_t>(job.in[j]);
+    for (unsigned i = 0; i < job.r; ++i) args[5 + job.k + i] = reinterpret_cast<uint64_t>(job.out[i]);
+    size_t size = args.size() * sizeof(uint64_t);
+    void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                      HIP_LAUNCH_PARAM_END};
+    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, 256, 1, 1, 0, stream, nullptr, config);
+    if (er == hipSuccess && name_out) *name_out = name;
+    return er;
+}
+
+}  // namespace zfec_hip

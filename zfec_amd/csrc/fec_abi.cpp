@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/zfec_hip.h"
+#include "bitslice.hpp"
 #include "gf256.hpp"
 #include "kernels.hpp"
 
@@ -676,6 +677,52 @@ FEC_API const char* fec_version(void) { return "zfec-hip 0.1.0 (gfx950)"; }
 FEC_API const char* fec_kernel_name(unsigned k, unsigned r) {
     if (k == 0 || r == 0 || k > static_cast<unsigned>(kMaxIn) || r > static_cast<unsigned>(kMaxOut)) return "split";
     return matapply_variant_name(k, r, false);
+}
+
+FEC_API const char* fec_last_kernel_name(void) { return matapply_last_kernel(); }
+
+FEC_API int fec_jit_mode(int mode) {
+    const int prev = static_cast<int>(jit_mode());
+    if (mode >= kJitOff && mode <= kJitForce) set_jit_mode(static_cast<JitMode>(mode));
+    set_status(FEC_OK);
+    return prev;
+}
+
+FEC_API int fec_jit_wait(void) {
+    set_status(FEC_OK);
+    return jit_wait();
+}
+
+namespace {
+// Compile the specialised kernels apply_matrix would launch for this r x k
+// matrix: its row groups of one launch each (codes with k <= kMaxIn; wider
+// codes run XOR-accumulating passes, which the table kernels serve).
+int prepare_rows(const uint8_t* coef, unsigned k, unsigned r) {
+    if (k > static_cast<unsigned>(kMaxIn) || r == 0) return set_status(FEC_OK);
+    const unsigned rmax = std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / k));
+    for (unsigned i0 = 0; i0 < r; i0 += rmax) {
+        const unsigned rg = std::min<unsigned>(rmax, r - i0);
+        if (jit_prepare(coef + size_t(i0) * k, k, rg) != 0)
+            return set_status(FEC_EHIP, "JIT compile failed: %s", jit_last_error().c_str());
+    }
+    return set_status(FEC_OK);
+}
+}  // namespace
+
+FEC_API int fec_jit_prepare_encode(const fec_t* code, const unsigned* block_nums, size_t num_block_nums) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
+    std::vector<uint8_t> rows;
+    encode_rows(code, block_nums, num_block_nums, rows);
+    return prepare_rows(rows.data(), code->k, static_cast<unsigned>(num_block_nums));
+}
+
+FEC_API int fec_jit_prepare_decode(const fec_t* code, const unsigned* index, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    std::vector<uint8_t> rows;
+    unsigned r = 0;
+    if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
+    return prepare_rows(rows.data(), code->k, r);
 }
 
 namespace {

@@ -34,6 +34,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "bitslice.hpp"
+
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -640,16 +642,29 @@ Variant* pick(uint32_t k, uint32_t r, bool acc) {
     return &g_lds_pad[(r + tiles - 1) / tiles];
 }
 
+thread_local const char* t_last_kernel = "";
+
 }  // namespace
 
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate) {
     return pick(k, r, accumulate)->name;
 }
 
+const char* matapply_last_kernel() { return t_last_kernel; }
+
 hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     if (job.k == 0 || job.k > static_cast<uint32_t>(kMaxIn) || job.r == 0 || job.r > static_cast<uint32_t>(kMaxOut) ||
         job.r * job.k > static_cast<uint32_t>(kMaxCoef) || job.nstripes == 0 || job.sz == 0)
         return hipErrorInvalidValue;
+    if (!job.tables) {  // a run-time specialised bit-sliced kernel, where one applies and is compiled
+        const char* jit_name = nullptr;
+        const hipError_t je = launch_matapply_jit(job, stream, &jit_name);
+        if (je == hipSuccess) {
+            t_last_kernel = jit_name;
+            return hipSuccess;
+        }
+        if (je != hipErrorNotSupported && je != hipErrorNotReady) return je;
+    }
     Variant* v = pick(job.k, job.r, job.accumulate != 0);
     const uint64_t cps = (job.sz + v->chunk - 1) / v->chunk;
     const uint64_t total = cps * job.nstripes;
@@ -685,6 +700,7 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
         job.tables = 1;
     }
     hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, job);
+    t_last_kernel = v->name;
     return hipGetLastError();
 }
 

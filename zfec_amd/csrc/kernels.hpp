@@ -47,7 +47,12 @@ constexpr int kMaxKernargTables = kMaxCoef / 4 / 5;  // 76 coefficients
 // otherwise); chooses the specialised variant for (k, r) when one exists.
 hipError_t launch_matapply(MatJob& job, hipStream_t stream);
 
-// Name of the variant launch_matapply would use (for tests / profiling).
+// Name of the table-kernel variant launch_matapply uses for (k, r) when no
+// run-time specialised kernel applies (for tests / profiling).
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
+
+// Name of the kernel the calling thread launched last (table variant or
+// bit-sliced JIT kernel, bitslice.hpp).
+const char* matapply_last_kernel();
 
 }  // namespace zfec_hip
