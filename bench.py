@@ -23,9 +23,8 @@ scaling).  cfg4/cfg5: the fixed batch is split by zfec_amd.shard.shard_range
 max/sum reductions.
 
 Also reported: the dominant kernel's roofline (encode: (k+r)*sz*stripes
-algorithmic HBM bytes per launch / median launch time over 50 encode/decode
-pairs launched as in the timed loop, with a HIP event pair around each launch
-on the launch stream; PMC traffic from
+algorithmic HBM bytes per launch / average launch duration over back-to-back
+launches between two HIP events on the launch stream; PMC traffic from
 profiles/pmc_summary.json), the decode kernel's, a batched 1 MiB-stripe
 encode (the north-star shape), and a bounded CPU baseline (rank 0, N=1) of
 the reference's own C code (oracle/_ref, kind "reference") or the oracle
@@ -288,9 +287,21 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
     barrier(dist)
     el = time.perf_counter() - t0
 
-    # Per-kernel launch duration for the roofline: the timed loop's own
-    # pattern (encode, decode, encode, ...) repeated with a HIP event pair
-    # around every launch on the launch stream; the median per kernel.
+    # Per-kernel launch duration for the roofline: `steps` back-to-back
+    # launches of one kernel between two HIP events on the launch stream
+    # (average duration, launch gaps included; what rocprof's kernel trace
+    # averages plus the gaps).  The interleaved per-launch event pairs of the
+    # timed loop's pattern are reported too (each interval also carries an
+    # event record).
+    def back_to_back(fn, n):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(n):
+            fn(stream.cuda_stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / n
+
     def per_launch(n=50):
         E = lambda: torch.cuda.Event(enable_timing=True)
         ev = [(E(), E(), E()) for _ in range(n)]
@@ -304,9 +315,12 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
         return (float(np.median([a.elapsed_time(b) for a, b, _ in ev])),
                 float(np.median([b.elapsed_time(c) for _, b, c in ev])))
 
+    nb = max(20, steps)
+    enc_b2b, dec_b2b = back_to_back(enc, nb), back_to_back(dec, nb)
     enc_ms, dec_ms = per_launch()
     return {"elapsed_s": el, "gpu_step_ms": e0.elapsed_time(e1) / steps, "launch": launch,
-            "enc_ms": enc_ms, "dec_ms": dec_ms, "nrec": nrec, "slots": slots, "kernels": kernels}
+            "enc_ms": enc_b2b, "dec_ms": dec_b2b, "enc_ms_pairs": enc_ms, "dec_ms_pairs": dec_ms, "b2b_launches": nb,
+            "nrec": nrec, "slots": slots, "kernels": kernels}
 
 
 def run_batched_1mib(steps):
@@ -385,10 +399,14 @@ def main():
                      "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),
                      "kernel": "%s (encode)" % t["kernels"]["encode"], "algorithmic_bytes_per_launch": enc_bytes,
                      "launch_ms": round(t["enc_ms"], 4),
-                     "timing": "median of 50 encode/decode pairs launched as in the timed loop, a HIP event pair around each launch on the launch stream"},
+                     "launch_ms_interleaved": round(t["enc_ms_pairs"], 4),
+                     "timing": "%d back-to-back encode launches between two HIP events on the launch stream "
+                               "(average launch duration); launch_ms_interleaved: median of 50 encode/decode pairs "
+                               "as in the timed loop, a HIP event pair around each launch" % t["b2b_launches"]},
         "decode_roofline": {"achieved": round(dec_ach, 1), "frac": round(dec_ach / HBM_PEAK_GBPS, 4),
                             "kernel": "%s (decode)" % t["kernels"]["decode"],
-                            "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4)},
+                            "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4),
+                            "launch_ms_interleaved": round(t["dec_ms_pairs"], 4)},
         "launch": t["launch"],
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
         "encode_input_GBps": round(k * sz * ns / (t["enc_ms"] * 1e-3) / 1e9, 1),

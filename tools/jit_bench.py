@@ -3,7 +3,8 @@
 (zfec_amd/csrc/bitslice.cpp) on device-resident stripes, interleaved rounds,
 medians.  Shapes: the bench workloads cfg3 (K=10/M=16, one 256 MiB stripe)
 and cfg4 (K=20/M=60, 1024 x 1 MiB stripes), encode and last-k decode.
-Variants: table kernels, JIT at tile heights 10/14/20, prefetch 1/2.
+Variants: table kernels, JIT at tile heights 10/14/20, prefetch 1/2, output
+store cache policies (nt / sc1 / sc0 sc1 / nt sc1).
 
 Per launch time = events around `reps` back-to-back launches on the launch
 stream / reps; HBM GB/s = (k + r) * sz * stripes / time.  Every variant's
@@ -31,9 +32,11 @@ VARIANTS = [
     ("jit_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14"}),
     ("jit_t20", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "20"}),
     ("jit_t14_pf2", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_PREFETCH": "2"}),
-    ("jit_t14_nobar", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_BARRIER": "0"}),
+    ("jit_t14_sc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "16"}),
+    ("jit_t14_sc0sc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "17"}),
+    ("jit_t14_ntsc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "18"}),
 ]
-KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER")
+KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE")
 
 
 def place(nums, k):

@@ -9,13 +9,12 @@ Reads gpurun_out/<tag>/<workload>/{ktrace,fetch,write}/*.csv (rocprofv3
   profiles/pmc_summary.json     {"encode_<workload>": ..., "decode_<workload>": ...}
                                 (read by bench.py for roofline.traffic)
 
-Roles come from dispatch order, which bench.py fixes (run_workload):
-(encode, decode) pairs from the first launch on: staging pair, warmup, 3,
-steps, 50 timed by per-launch events.  Encode and decode of one workload can
-be the same kernel at the same grid (K=10/M=16 decodes 6 rows, as it encodes
-6), so names alone do not tell them apart.  Per role only the launches of its
-most frequent kernel count: the first launches of a wide code run the table
-kernel while its bit-sliced kernel compiles (zfec_amd/csrc/bitslice.cpp).
+Roles come from kernel names: bench.py prints the encode and decode kernels it
+timed (roofline.kernel / decode_roofline.kernel in its JSON line, captured in
+ktrace.log); launches of other kernels (the table kernels that run while a
+bit-sliced kernel compiles, torch's own) are left out.  When encode and decode
+are the same kernel (one table variant for both), its launches are reported
+once as "encode+decode".
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE (KiB) reads exactly half
 of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is
@@ -40,8 +39,38 @@ def load(path):
         return list(csv.DictReader(f))
 
 
-def roles(n):
-    return ["encode" if i % 2 == 0 else "decode" for i in range(n)]
+def bench_kernels(src):
+    """(encode, decode) kernel names from the bench JSON line in ktrace.log."""
+    with open(os.path.join(src, "ktrace.log")) as f:
+        line = [l for l in f if l.startswith("{")][-1]
+    d = json.loads(line)
+    strip = lambda s: s.rsplit(" (", 1)[0]
+    return strip(d["roofline"]["kernel"]), strip(d["decode_roofline"]["kernel"])
+
+
+def role_of(name, enc, dec):
+    n = short(name)
+    if enc == dec:
+        return "encode+decode" if n.startswith(enc.split("<")[0]) and _same(n, enc) else None
+    if _same(n, enc):
+        return "encode"
+    if _same(n, dec):
+        return "decode"
+    return None
+
+
+def _same(traced, printed):
+    """rocprof's demangled template name vs the library's short variant name."""
+    if traced == printed:
+        return True
+    # matapply_reg<3, 7, true, 1> vs matapply_reg<3,7>; matapply_lds<false, true, 6, 2, 2, 1> vs matapply_lds<6,2,2,pad>
+    base_t, base_p = traced.split("<")[0], printed.split("<")[0]
+    if base_t != base_p or "<" not in traced:
+        return False
+    targs = [a.strip() for a in traced.split("<", 1)[1].rstrip(">").split(",")]
+    pargs = [a.strip() for a in printed.split("<", 1)[1].rstrip(">").split(",") if a.strip() != "pad"]
+    nums = [a for a in targs if a.lstrip("-").isdigit()]
+    return nums[:len(pargs)] == pargs
 
 
 def ours(rows):
@@ -57,27 +86,23 @@ def counter_rows(d):
 
 
 def summarize(src):
+    enc, dec = bench_kernels(src)
     kt = ours(load(os.path.join(src, "ktrace", "kt_kernel_trace.csv")))
     fe = counter_rows(os.path.join(src, "fetch"))
     wr = counter_rows(os.path.join(src, "write"))
     res = {}
     for rows, col in ((kt, "dur_ns"), (fe, "fetch_kib"), (wr, "write_kib")):
-        for r, role in zip(rows, roles(len(rows))):
-            e = res.setdefault(role, {"kernel": "", "names": [], "dur_ns": [], "fetch_kib": [], "write_kib": [],
-                                      "names_dur_ns": [], "names_fetch_kib": [], "names_write_kib": []})
-            e["names_" + col].append(r["Kernel_Name"])
+        for r in rows:
+            role = role_of(r["Kernel_Name"], enc, dec)
+            if role is None:
+                continue
+            e = res.setdefault(role, {"kernel": short(r["Kernel_Name"]), "dur_ns": [], "fetch_kib": [], "write_kib": []})
             if col == "dur_ns":
-                e["names"].append(r["Kernel_Name"])
                 e[col].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             else:
                 e[col].append(float(r["Counter_Value"]))
     out = {}
     for role, e in res.items():
-        names = e.pop("names")
-        main = max(set(names), key=names.count)
-        for col in ("dur_ns", "fetch_kib", "write_kib"):
-            e[col] = [v for v, nm in zip(e[col], e["names_" + col]) if nm == main]
-        e["kernel"] = short(main)
         mean = lambda v: sum(v) / len(v) if v else None
         fetch, write = mean(e["fetch_kib"]), mean(e["write_kib"])
         out[role] = {"kernel": e["kernel"], "launches": len(e["dur_ns"]),

@@ -89,7 +89,8 @@ __device__ __forceinline__ void tr8(u32& v0, u32& v1, u32& v2, u32& v3, u32& v4,
 }
 // Buffer loads / stores off a wave-uniform base (block pointer + the unit's
 // offset, in SGPRs) with the lane's 32-bit offset: no 64-bit VGPR address per
-// block.  aux 2 = nt (streaming store).
+// block.  Store cache policy kStoreAux: 2 = nt (streaming), 16 = sc1,
+// 17 = sc0 sc1, 18 = nt sc1.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const u8* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(p), (short)0, -1, 0x00020000);
 }
@@ -97,7 +98,7 @@ __device__ __forceinline__ u32x4 ld(__amdgpu_buffer_rsrc_t r, u32 off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, u32 off, u32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
 }
 )";
 
@@ -139,6 +140,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
 
     Src e;
     e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
+    e("constexpr int kStoreAux = %u;\n", opt.store_aux);
     e.s += kPrelude;
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
     e("extern \"C\" __global__ __launch_bounds__(256) void %s(const Args a) {\n", name);
@@ -429,6 +431,7 @@ BsOptions options_from_env() {
     o.prefetch = env_uint("ZFEC_HIP_JIT_PREFETCH", o.prefetch);
     if (o.prefetch > 4) o.prefetch = 4;
     o.barriers = env_uint("ZFEC_HIP_JIT_BARRIER", 1) != 0;
+    o.store_aux = env_uint("ZFEC_HIP_JIT_STORE", o.store_aux) & 0x1Fu;
     return o;
 }
 
@@ -440,7 +443,8 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     std::string key;
     key.reserve(32 + size_t(k) * r);
     char hdr[64];
-    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0);
+    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
+             opt.store_aux);
     key += hdr;
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     auto it = R.entries.find(key);

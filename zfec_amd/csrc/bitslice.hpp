@@ -32,6 +32,7 @@ struct BsOptions {
     unsigned max_tile = kBsMaxTile;  // rows per tile (tiles are near-equal)
     unsigned prefetch = 1;           // input steps loaded ahead of the one being computed
     bool barriers = true;            // sched_barrier between input steps (keeps the prefetch shape)
+    unsigned store_aux = 2;          // cache policy bits of the output stores (2 = nt)
 };
 
 // Source of the kernel `name` for the r x k matrix `coef` (row-major).

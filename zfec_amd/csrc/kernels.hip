@@ -157,6 +157,22 @@ __device__ __forceinline__ void store16_out(uint8_t* p, u32x4 v) {
         store16(p, v);
 }
 
+// Output store with an explicit cache policy (SP != 0; tools/mb_store.hip):
+// 1 = sc1, 2 = sc0 sc1, 3 = nt sc1.  SP = 0 defers to store16_out<NT>.  The
+// trailing s_nop keeps the compiler's next instruction from overwriting the
+// data registers before the store has read them.
+template <bool NT, int SP>
+__device__ __forceinline__ void store16_pol(uint8_t* p, u32x4 v) {
+    if constexpr (SP == 1)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 2)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 3)
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else
+        store16_out<NT>(p, v);
+}
+
 // The last (sz % 16) bytes of a block.
 __device__ inline u32x4 load_tail(const uint8_t* p, uint32_t nb) {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -214,7 +230,7 @@ __device__ __forceinline__ Span chunk_span(uint32_t c, uint64_t sz, uint32_t nfu
 // words in SGPRs and copies the low words to VGPRs once, outside the loop.
 // ---------------------------------------------------------------------------
 // One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.
-template <int K, int R, bool NT>
+template <int K, int R, bool NT, int SP = 0>
 __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
                                                   uint64_t ob, bool full, uint32_t nb) {
     Sel sel[4][K];
@@ -230,7 +246,7 @@ __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (
         const u32x4 y{gf_dot<K>(T[r], sel[0]), gf_dot<K>(T[r], sel[1]), gf_dot<K>(T[r], sel[2]),
                       gf_dot<K>(T[r], sel[3])};
         if (full)
-            store16_out<NT>(job.out[r] + ob, y);
+            store16_pol<NT, SP>(job.out[r] + ob, y);
         else
             store_tail(job.out[r] + ob, y, nb);
     }
@@ -248,7 +264,7 @@ __device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint6
 }
 
 // U: units per lane per loop trip (U = 2 puts 2K loads in flight per lane).
-template <int K, int R, bool NT, int U = 1>
+template <int K, int R, bool NT, int U = 1, int SP = 0>
 __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
     Tab T[R][K];
 #pragma unroll
@@ -277,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
         }
 #pragma unroll
         for (int i = 0; i < U; ++i)
-            if (live[i]) reg_compute_store<K, R, NT>(job, T, x[i], ob[i], full[i], nb[i]);
+            if (live[i]) reg_compute_store<K, R, NT, SP>(job, T, x[i], ob[i], full[i], nb[i]);
     }
 }
 
