@@ -39,8 +39,8 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-# (k, m): few/many inputs and outputs, one and several register tiles
-JIT_SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40)]
+# (k, m): few/many inputs and outputs; one row tile, or 2-5 tiles on the waves of a workgroup
+JIT_SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (10, 58)]
 
 
 @pytest.mark.parametrize("k,m", JIT_SHAPES)

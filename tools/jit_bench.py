@@ -3,8 +3,11 @@
 (zfec_amd/csrc/bitslice.cpp) on device-resident stripes, interleaved rounds,
 medians.  Shapes: the bench workloads cfg3 (K=10/M=16, one 256 MiB stripe)
 and cfg4 (K=20/M=60, 1024 x 1 MiB stripes), encode and last-k decode.
-Variants: table kernels, JIT at tile heights 10/14/20, prefetch 1/2, output
-store cache policies (nt / sc1 / sc0 sc1 / nt sc1).
+Variants (ZFEC_HIP_JIT_* knobs): table kernels; bit-sliced JIT kernels with
+the default options, Gray-code combination order, waves-per-SIMD register
+bounds, row tiles split across the waves of a workgroup (ZFEC_HIP_JIT_SPLIT)
+at several tile heights, prefetch 2.  (Earlier rounds of this A/B: tile
+heights 10/14/20, store cache policies; profiles/r01_jit_ab.log.)
 
 Per launch time = events around `reps` back-to-back launches on the launch
 stream / reps; HBM GB/s = (k + r) * sz * stripes / time.  Every variant's
@@ -28,15 +31,16 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
 VARIANTS = [
     ("table", capi.JIT_OFF, {}),
-    ("jit_t10", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "10"}),
-    ("jit_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14"}),
-    ("jit_t20", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "20"}),
-    ("jit_t14_pf2", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_PREFETCH": "2"}),
-    ("jit_t14_sc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "16"}),
-    ("jit_t14_sc0sc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "17"}),
-    ("jit_t14_ntsc1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_STORE": "18"}),
+    ("jit_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "0", "ZFEC_HIP_JIT_TILE": "14"}),
+    ("jit_t14_w3", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "0", "ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_WAVES": "3"}),
+    ("split_t10", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10"}),
+    ("split_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "14"}),
+    ("split_t10_pf2", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10", "ZFEC_HIP_JIT_PREFETCH": "2"}),
+    ("split_t10_gray", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10", "ZFEC_HIP_JIT_ORDER": "1"}),
+    ("split_t7", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "7"}),
 ]
-KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE")
+KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE",
+         "ZFEC_HIP_JIT_ORDER", "ZFEC_HIP_JIT_WAVES", "ZFEC_HIP_JIT_SPLIT")
 
 
 def place(nums, k):

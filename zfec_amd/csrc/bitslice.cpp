@@ -128,10 +128,19 @@ struct Combos {
 
 }  // namespace
 
+unsigned bitslice_tiles(unsigned r, const BsOptions& opt) {
+    const unsigned maxt = opt.max_tile ? opt.max_tile : kBsMaxTile;
+    return (r + maxt - 1) / maxt;
+}
+
+bool bitslice_split(unsigned r, const BsOptions& opt) {
+    const unsigned nt = bitslice_tiles(r, opt);
+    return opt.split && nt > 1 && nt <= 8;
+}
+
 std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name) {
     field_init();
-    const unsigned maxt = opt.max_tile ? opt.max_tile : kBsMaxTile;
-    const unsigned ntiles = (r + maxt - 1) / maxt;
+    const unsigned ntiles = bitslice_tiles(r, opt);
     std::vector<unsigned> tile_lo(ntiles + 1);
     for (unsigned t = 0; t <= ntiles; ++t) tile_lo[t] = t * r / ntiles;  // near-equal tiles
     std::vector<uint8_t> masks(size_t(r) * k * 8);
@@ -143,9 +152,22 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     e("constexpr int kStoreAux = %u;\n", opt.store_aux);
     e.s += kPrelude;
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
-    e("extern \"C\" __global__ __launch_bounds__(256) void %s(const Args a) {\n", name);
+    // split: the row tiles of a unit go to the waves of one workgroup, which
+    // read the unit's inputs at the same time (L1/L2 hits instead of a re-read
+    // from HBM per tile); otherwise each wave walks all tiles of its own unit.
+    const bool split = bitslice_split(r, opt);
+    const unsigned threads = split ? 64 * ntiles : 256;
+    if (opt.waves)
+        e("extern \"C\" __global__ __launch_bounds__(%u, %u) void %s(const Args a) {\n", threads, opt.waves, name);
+    else
+        e("extern \"C\" __global__ __launch_bounds__(%u) void %s(const Args a) {\n", threads, name);
     e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n");
-    e("  const u32 wid = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
+    if (split) {
+        e("  const u32 tile = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
+        e("  const u32 wid = blockIdx.x;\n");
+    } else {
+        e("  const u32 wid = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
+    }
     e("  u32 s = wid / a.cps, c = wid - s * a.cps;\n");
     e("  while (s < a.nstripes) {\n");
     e("    u64 off = (u64)c * %uu;\n", kBsChunk);
@@ -153,7 +175,8 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
       kBsChunk, kBsChunk);
     e("    const u64 ub = (u64)s * a.iss + off, uo = (u64)s * a.oss + off;\n");
 
-    // Steps: (tile t, input j) in order; loads run `prefetch` steps ahead.
+    // Steps: (tile t, input j) in order; loads run `prefetch` steps ahead
+    // (across tiles, or inside each tile when split).
     const unsigned nsteps = ntiles * k;
     const unsigned pf = opt.prefetch;
     auto emit_load = [&](unsigned n) {
@@ -161,10 +184,16 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         e("    const __amdgpu_buffer_rsrc_t ri%u = rs(a.in[%u] + ub);\n", n, j);
         e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", n, n, n, n);
     };
-    for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
+    if (!split)
+        for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
     for (unsigned t = 0; t < ntiles; ++t) {
         const unsigned r0 = tile_lo[t], r1 = tile_lo[t + 1];
+        const unsigned seq_end = split ? (t + 1) * k : nsteps;  // prefetch horizon
         e("    // tile %u: rows %u..%u\n", t, r0, r1 - 1);
+        if (split) {
+            e("    if (tile == %uu) {\n", t);
+            for (unsigned n = t * k; n < t * k + pf && n < seq_end; ++n) emit_load(n);
+        }
         std::vector<char> init(size_t(r1 - r0) * 8, 0);
         for (unsigned i = r0; i < r1; ++i)
             e("    u32 a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7;\n", i, i, i, i, i, i, i, i);
@@ -172,34 +201,68 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             const unsigned n = t * k + j;
             if (pf == 0)
                 emit_load(n);
-            else if (n + pf < nsteps)
+            else if (n + pf < seq_end)
                 emit_load(n + pf);
             e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", n, n, n, n, n, n, n, n);
             e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", n, n, n, n, n, n, n, n);
             e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
             Combos lo{n, 'L', 0}, hi{n, 'H', 4};
+            struct Upd {
+                unsigned i, b, ml, mh;
+            };
+            std::vector<Upd> ups;
             for (unsigned i = r0; i < r1; ++i) {
                 const uint8_t* mk = &masks[(size_t(i) * k + j) * 8];
-                for (unsigned b = 0; b < 8; ++b) {
-                    const unsigned m = mk[b];
-                    if (!m) continue;
-                    char acc[32];
-                    snprintf(acc, sizeof acc, "a%u_%u", i, b);
-                    char& ini = init[size_t(i - r0) * 8 + b];
-                    const unsigned ml = m & 15u, mh = m >> 4;
-                    const std::string sl = ml ? lo.name(ml, e) : std::string();
-                    const std::string sh = mh ? hi.name(mh, e) : std::string();
-                    if (!ini) {
-                        if (ml && mh)
-                            e("    %s = %s ^ %s;\n", acc, sl.c_str(), sh.c_str());
-                        else
-                            e("    %s = %s;\n", acc, ml ? sl.c_str() : sh.c_str());
-                        ini = 1;
-                    } else if (ml && mh) {
-                        e("    %s = x3(%s, %s, %s);\n", acc, acc, sl.c_str(), sh.c_str());
+                for (unsigned b = 0; b < 8; ++b)
+                    if (mk[b]) ups.push_back(Upd{i, b, mk[b] & 15u, unsigned(mk[b]) >> 4});
+            }
+            auto update = [&](const Upd& u, const std::string& sl, const std::string& sh) {
+                char acc[32];
+                snprintf(acc, sizeof acc, "a%u_%u", u.i, u.b);
+                char& ini = init[size_t(u.i - r0) * 8 + u.b];
+                if (!ini) {
+                    if (u.ml && u.mh)
+                        e("    %s = %s ^ %s;\n", acc, sl.c_str(), sh.c_str());
+                    else
+                        e("    %s = %s;\n", acc, u.ml ? sl.c_str() : sh.c_str());
+                    ini = 1;
+                } else if (u.ml && u.mh) {
+                    e("    %s = x3(%s, %s, %s);\n", acc, acc, sl.c_str(), sh.c_str());
+                } else {
+                    e("    %s ^= %s;\n", acc, u.ml ? sl.c_str() : sh.c_str());
+                }
+            };
+            if (!opt.gray) {  // combinations on first use, in row order
+                for (const Upd& u : ups)
+                    update(u, u.ml ? lo.name(u.ml, e) : std::string(), u.mh ? hi.name(u.mh, e) : std::string());
+            } else {
+                // H combinations stay live for the step; L values are walked in
+                // Gray-code order (one XOR from the previous one), so only the
+                // current one is live while the updates that use it run
+                for (const Upd& u : ups)
+                    if (!u.ml) update(u, std::string(), hi.name(u.mh, e));
+                static const unsigned kGray[15] = {1, 3, 2, 6, 7, 5, 4, 12, 13, 15, 14, 10, 11, 9, 8};
+                int last = -1;
+                for (int g = 0; g < 15; ++g)
+                    for (const Upd& u : ups)
+                        if (u.ml == kGray[g]) last = g;
+                std::string prev;
+                for (int g = 0; g <= last; ++g) {
+                    const unsigned m = kGray[g];
+                    std::string cur;
+                    char nm[32];
+                    if ((m & (m - 1)) == 0) {
+                        snprintf(nm, sizeof nm, "q%u_%u", n, unsigned(__builtin_ctz(m)));
+                        cur = nm;
                     } else {
-                        e("    %s ^= %s;\n", acc, ml ? sl.c_str() : sh.c_str());
+                        const unsigned bit = m ^ kGray[g - 1];
+                        snprintf(nm, sizeof nm, "G%u_%u", n, m);
+                        e("    const u32 %s = %s ^ q%u_%u;\n", nm, prev.c_str(), n, unsigned(__builtin_ctz(bit)));
+                        cur = nm;
                     }
+                    for (const Upd& u : ups)
+                        if (u.ml == m) update(u, cur, u.mh ? hi.name(u.mh, e) : std::string());
+                    prev = cur;
                 }
             }
             if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
@@ -212,6 +275,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
             e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
         }
+        if (split) e("    }\n");
     }
     e("    c += a.gs_c;\n    s += a.gs_s;\n    if (c >= a.cps) { c -= a.cps; ++s; }\n  }\n}\n");
     return e.s;
@@ -322,6 +386,10 @@ bool compile_code(const std::string& src, const std::string& name, std::vector<c
     const std::string dir = cache_dir();
     const std::string path = dir.empty() ? std::string() : dir + "/" + name + "-" + hex + ".co";
     if (!path.empty() && read_file(path, code)) return true;
+    if (const char* d = getenv("ZFEC_HIP_JIT_DUMP")) {  // the generated source, for offline inspection
+        std::vector<char> text(src.begin(), src.end());
+        write_file_atomic(std::string(d) + "/" + name + ".hip", text);
+    }
     const Rtc& R = rtc();
     if (!R.ok) {
         err = R.err;
@@ -368,6 +436,8 @@ struct Loaded {
 struct Entry {
     int state = 0;  // 0 compiling, 1 ready, 2 failed
     std::string name;
+    unsigned threads = 256;          // workgroup size
+    unsigned units_per_block = 4;    // units a workgroup covers per loop trip
     std::vector<char> code;
     std::map<int, Loaded> dev;
 };
@@ -432,6 +502,10 @@ BsOptions options_from_env() {
     if (o.prefetch > 4) o.prefetch = 4;
     o.barriers = env_uint("ZFEC_HIP_JIT_BARRIER", 1) != 0;
     o.store_aux = env_uint("ZFEC_HIP_JIT_STORE", o.store_aux) & 0x1Fu;
+    o.gray = env_uint("ZFEC_HIP_JIT_ORDER", o.gray ? 1 : 0) != 0;
+    o.waves = env_uint("ZFEC_HIP_JIT_WAVES", o.waves);
+    o.split = env_uint("ZFEC_HIP_JIT_SPLIT", o.split ? 1 : 0) != 0;
+    if (o.waves > 8) o.waves = 8;
     return o;
 }
 
@@ -443,8 +517,8 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     std::string key;
     key.reserve(32 + size_t(k) * r);
     char hdr[64];
-    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
-             opt.store_aux);
+    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
+             opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
     key += hdr;
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     auto it = R.entries.find(key);
@@ -454,6 +528,8 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     char nm[80];
     snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
     e->name = nm;
+    e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
+    e->units_per_block = bitslice_split(r, opt) ? 1 : 4;
     R.entries.emplace(key, std::move(ne));
     ++R.pending;
     std::string src = bitslice_source(coef, k, r, opt, nm);
@@ -547,7 +623,9 @@ hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char
             return hipErrorNotSupported;
         }
         int nb = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.fn, 256, 0) == hipSuccess && nb > 0)
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.fn, static_cast<int>(e->threads), 0) ==
+                hipSuccess &&
+            nb > 0)
             L.blocks_per_cu = nb;
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
@@ -556,15 +634,16 @@ hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char
     }
     const Loaded L = it->second;
     const char* name = e->name.c_str();  // stable: entries are never removed
+    const unsigned threads = e->threads, upb = e->units_per_block;
     lk.unlock();
 
     const uint64_t cps = (job.sz + kBsChunk - 1) / kBsChunk;
     const uint64_t waves = cps * job.nstripes;
     if (waves >= (1ull << 32) - (1ull << 24)) return hipErrorNotSupported;
-    const uint64_t need = (waves + 3) / 4;
+    const uint64_t need = (waves + upb - 1) / upb;
     const uint64_t cap = uint64_t(L.num_cu) * L.blocks_per_cu * 64;
     const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
-    const uint64_t gwaves = uint64_t(grid) * 4;
+    const uint64_t gwaves = uint64_t(grid) * upb;  // units per grid-stride step
     // struct Args of the generated source: 3 x u64, 4 x u32, k + r pointers
     std::vector<uint64_t> args(5 + job.k + job.r);
     args[0] = job.sz;
@@ -578,7 +657,7 @@ hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char
     size_t size = args.size() * sizeof(uint64_t);
     void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                       HIP_LAUNCH_PARAM_END};
-    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, 256, 1, 1, 0, stream, nullptr, config);
+    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, 0, stream, nullptr, config);
     if (er == hipSuccess && name_out) *name_out = name;
     return er;
 }

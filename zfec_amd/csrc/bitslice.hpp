@@ -26,14 +26,22 @@
 namespace zfec_hip {
 
 constexpr int kBsChunk = 2048;    // bytes of a block per wave per unit (32 per lane, two 1 KiB halves)
-constexpr int kBsMaxTile = 14;    // output rows per register tile (8 accumulator planes each)
+constexpr int kBsMaxTile = 10;    // output rows per register tile (8 accumulator planes each)
 
 struct BsOptions {
     unsigned max_tile = kBsMaxTile;  // rows per tile (tiles are near-equal)
-    unsigned prefetch = 1;           // input steps loaded ahead of the one being computed
+    unsigned prefetch = 2;           // input steps loaded ahead of the one being computed
     bool barriers = true;            // sched_barrier between input steps (keeps the prefetch shape)
     unsigned store_aux = 2;          // cache policy bits of the output stores (2 = nt)
+    bool gray = false;               // walk the planes-0-3 combinations in Gray-code order
+    unsigned waves = 0;              // __launch_bounds__ waves-per-SIMD hint (0: none)
+    bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
 };
+
+// Row tiles of an r-row matrix, and whether they go to the waves of one
+// workgroup (2-8 tiles) or each wave walks all of them.
+unsigned bitslice_tiles(unsigned r, const BsOptions& opt);
+bool bitslice_split(unsigned r, const BsOptions& opt);
 
 // Source of the kernel `name` for the r x k matrix `coef` (row-major).
 std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name);
