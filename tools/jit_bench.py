@@ -5,9 +5,10 @@ medians.  Shapes: the bench workloads cfg3 (K=10/M=16, one 256 MiB stripe)
 and cfg4 (K=20/M=60, 1024 x 1 MiB stripes), encode and last-k decode.
 Variants (ZFEC_HIP_JIT_* knobs): table kernels; bit-sliced JIT kernels with
 the default options, Gray-code combination order, waves-per-SIMD register
-bounds, row tiles split across the waves of a workgroup (ZFEC_HIP_JIT_SPLIT)
-at several tile heights, prefetch 2.  (Earlier rounds of this A/B: tile
-heights 10/14/20, store cache policies; profiles/r01_jit_ab.log.)
+bounds, row tiles split across the waves of a workgroup, bit-planes shared
+through LDS (ZFEC_HIP_JIT_SHARE) at several tile heights.  Earlier rounds of
+this A/B: profiles/r01_jit_ab.log (tile heights, store cache policies),
+profiles/r01_jit_ab2.log (split).
 
 Per launch time = events around `reps` back-to-back launches on the launch
 stream / reps; HBM GB/s = (k + r) * sz * stripes / time.  Every variant's
@@ -31,16 +32,15 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
 VARIANTS = [
     ("table", capi.JIT_OFF, {}),
-    ("jit_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "0", "ZFEC_HIP_JIT_TILE": "14"}),
-    ("jit_t14_w3", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "0", "ZFEC_HIP_JIT_TILE": "14", "ZFEC_HIP_JIT_WAVES": "3"}),
-    ("split_t10", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10"}),
-    ("split_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "14"}),
-    ("split_t10_pf2", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10", "ZFEC_HIP_JIT_PREFETCH": "2"}),
-    ("split_t10_gray", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "10", "ZFEC_HIP_JIT_ORDER": "1"}),
-    ("split_t7", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SPLIT": "1", "ZFEC_HIP_JIT_TILE": "7"}),
+    ("split", capi.JIT_FORCE, {}),
+    ("share", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1"}),
+    ("share_pf1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "1"}),
+    ("share_t14", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_TILE": "14"}),
+    ("share_t8", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_TILE": "8"}),
+    ("share_gray", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_ORDER": "1"}),
 ]
 KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE",
-         "ZFEC_HIP_JIT_ORDER", "ZFEC_HIP_JIT_WAVES", "ZFEC_HIP_JIT_SPLIT")
+         "ZFEC_HIP_JIT_ORDER", "ZFEC_HIP_JIT_WAVES", "ZFEC_HIP_JIT_SPLIT", "ZFEC_HIP_JIT_SHARE")
 
 
 def place(nums, k):

@@ -162,6 +162,10 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     else
         e("extern \"C\" __global__ __launch_bounds__(%u) void %s(const Args a) {\n", threads, name);
     e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n");
+    if (split && opt.share) {
+        e("  __shared__ u32x4 sh[%u];  // [input][half][lane] bit-planes of the unit\n", k * 128);
+        e("  const u32 lane = threadIdx.x & 63u;\n");
+    }
     if (split) {
         e("  const u32 tile = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
         e("  const u32 wid = blockIdx.x;\n");
@@ -179,13 +183,42 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // (across tiles, or inside each tile when split).
     const unsigned nsteps = ntiles * k;
     const unsigned pf = opt.prefetch;
+    // share: each wave of the workgroup loads and transposes k / ntiles of the
+    // unit's inputs once and leaves their bit-planes in LDS for all waves
+    const bool share = split && opt.share;
     auto emit_load = [&](unsigned n) {
         const unsigned j = n % k;
+        if (share) {
+            e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, j * 128, n, j * 128 + 64);
+            return;
+        }
         e("    const __amdgpu_buffer_rsrc_t ri%u = rs(a.in[%u] + ub);\n", n, j);
         e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", n, n, n, n);
     };
     if (!split)
         for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
+    if (share) {
+        e("    // inputs -> bit-planes -> LDS, k / %u per wave\n", ntiles);
+        for (unsigned t = 0; t < ntiles; ++t) {
+            if (t >= k) break;
+            e("    if (tile == %uu) {\n", t);
+            for (unsigned j = t; j < k; j += ntiles) {
+                e("      const __amdgpu_buffer_rsrc_t pi%u = rs(a.in[%u] + ub);\n", j, j);
+                e("      const u32x4 p%u_0 = ld(pi%u, lo16), p%u_1 = ld(pi%u, lo16 + 1024u);\n", j, j, j, j);
+            }
+            for (unsigned j = t; j < k; j += ntiles) {
+                e("      u32 w%u_0 = p%u_0.x, w%u_1 = p%u_0.y, w%u_2 = p%u_0.z, w%u_3 = p%u_0.w;\n", j, j, j, j, j, j, j,
+                  j);
+                e("      u32 w%u_4 = p%u_1.x, w%u_5 = p%u_1.y, w%u_6 = p%u_1.z, w%u_7 = p%u_1.w;\n", j, j, j, j, j, j, j,
+                  j);
+                e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
+                e("      sh[%uu + lane] = u32x4{w%u_0, w%u_1, w%u_2, w%u_3};\n", j * 128, j, j, j, j);
+                e("      sh[%uu + lane] = u32x4{w%u_4, w%u_5, w%u_6, w%u_7};\n", j * 128 + 64, j, j, j, j);
+            }
+            e("    }\n");
+        }
+        e("    __syncthreads();\n");
+    }
     for (unsigned t = 0; t < ntiles; ++t) {
         const unsigned r0 = tile_lo[t], r1 = tile_lo[t + 1];
         const unsigned seq_end = split ? (t + 1) * k : nsteps;  // prefetch horizon
@@ -205,7 +238,8 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                 emit_load(n + pf);
             e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", n, n, n, n, n, n, n, n);
             e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", n, n, n, n, n, n, n, n);
-            e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
+            if (!share)  // LDS holds planes already
+                e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
             Combos lo{n, 'L', 0}, hi{n, 'H', 4};
             struct Upd {
                 unsigned i, b, ml, mh;
@@ -277,6 +311,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         }
         if (split) e("    }\n");
     }
+    if (share) e("    __syncthreads();  // every wave has read the planes before the next unit's overwrite\n");
     e("    c += a.gs_c;\n    s += a.gs_s;\n    if (c >= a.cps) { c -= a.cps; ++s; }\n  }\n}\n");
     return e.s;
 }
@@ -505,6 +540,7 @@ BsOptions options_from_env() {
     o.gray = env_uint("ZFEC_HIP_JIT_ORDER", o.gray ? 1 : 0) != 0;
     o.waves = env_uint("ZFEC_HIP_JIT_WAVES", o.waves);
     o.split = env_uint("ZFEC_HIP_JIT_SPLIT", o.split ? 1 : 0) != 0;
+    o.share = env_uint("ZFEC_HIP_JIT_SHARE", o.share ? 1 : 0) != 0;
     if (o.waves > 8) o.waves = 8;
     return o;
 }
@@ -519,6 +555,7 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     char hdr[64];
     snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
              opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
+    if (opt.share && bitslice_split(r, opt)) key += "share/";
     key += hdr;
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     auto it = R.entries.find(key);

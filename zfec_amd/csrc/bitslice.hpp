@@ -36,6 +36,7 @@ struct BsOptions {
     bool gray = false;               // walk the planes-0-3 combinations in Gray-code order
     unsigned waves = 0;              // __launch_bounds__ waves-per-SIMD hint (0: none)
     bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
+    bool share = true;               // split: inputs transposed once per unit, bit-planes shared through LDS
 };
 
 // Row tiles of an r-row matrix, and whether they go to the waves of one
