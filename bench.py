@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip the 1 MiB-stripe batched leg")
+    p.add_argument("--layout", default="256", choices=["odd128", "256"],
+                   help="block row stride in HBM: 256-byte multiple (default) or an odd number of 128-byte lines")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -102,6 +104,18 @@ def reduce(dist, x, op):
 
 def align_up(x, a):
     return (x + a - 1) // a * a
+
+
+def row_stride(sz, rule="256"):
+    """Distance between consecutive block rows in HBM.  "256": rows rounded up
+    to 256 bytes (default).  "odd128": an odd number of 128-byte lines (in the
+    kernel microbenchmark, tools/mb_encode.exe MB_BATCH with 1366-byte rows, 4.78
+    vs 4.41 TB/s; in this bench's encode+decode step no difference on any
+    workload, 2 runs each)."""
+    if rule == "256":
+        return align_up(sz, 256)
+    lines = -(-sz // 128)
+    return 128 * (lines if lines % 2 else lines + 1)
 
 
 def place(nums, k):
@@ -209,14 +223,14 @@ def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
     return {key: round(v, 1) for key, v in res.items()}
 
 
-def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False):
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256"):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
-    to 256 bytes, so every block starts 256-byte aligned (the reference's API
-    takes separate buffers per block, which are aligned too)."""
+    to 256 bytes (row_stride), so every block starts 256-byte aligned (the
+    reference's API takes separate buffers per block, which are aligned too)."""
     r = m - k
-    ld = align_up(sz, 256)
+    ld = row_stride(sz, layout)
     gen = torch.Generator(device="cuda").manual_seed(1234 + k)
     data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen)
     par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
@@ -328,7 +342,7 @@ def run_batched_1mib(steps):
     launch (block rows 256-byte aligned, as in the main workload)."""
     k, m, ns = 3, 10, 256
     sz = -(-(1 << 20) // k)
-    ld = align_up(sz, 256)
+    ld = row_stride(sz)
     code = capi.Code(k, m)
     src = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda")
     dst = torch.empty((ns, m - k, ld), dtype=torch.uint8, device="cuda")
@@ -365,7 +379,7 @@ def main():
         ns = s1 - s0
     else:
         ns = nstripes
-    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph)
+    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
     value = total_bytes / el / 1e9
@@ -393,7 +407,7 @@ def main():
         "data": "synthetic (torch.randint bytes, resident in HBM)",
         "config": {"workload": "%s: encode (%d->%d blocks) + decode from blocks %s" % (desc, k, r, t["slots"]),
                    "name": args.workload, "k": k, "m": m, "stripe_bytes": stripe, "stripes_per_gpu": ns,
-                   "block_bytes": sz, "block_row_stride": align_up(sz, 256),
+                   "block_bytes": sz, "block_row_stride": row_stride(sz, args.layout),
                    "parallelism": "stripes sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": round(enc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),

@@ -1,6 +1,7 @@
 // mb_encode.hip -- microbenchmark of the matrix-apply kernels on one GPU.
 //
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_encode.hip -o tools/mb_encode.exe
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_encode.hip zfec_amd/csrc/bitslice.cpp \
+//          zfec_amd/csrc/gf256.cpp -ldl -o tools/mb_encode.exe
 // Run:   ./tools/mb_encode.exe [stripe_bytes]
 //
 // 1. A copy-shaped ceiling kernel that moves the K=3/M=10 encode's bytes
