@@ -208,3 +208,29 @@ def test_no_gpu_fails_loudly():
         zfec_amd.Decoder(3, 10).decode([b"abc", b"def", b"ghi"], [3, 4, 5])
     with pytest.raises(zfec_amd.Error, match="no GPU"):
         zfec_amd.test_from_agl()
+
+
+def test_jit_prepare_concurrent_threads(tmp_path, monkeypatch):
+    """Several threads asking for the same and for different kernels at once
+    (ctypes releases the GIL): one compile per matrix, every call succeeds."""
+    import threading
+
+    monkeypatch.setenv("ZFEC_HIP_JIT_CACHE", str(tmp_path))
+    codes = {km: capi.Code(*km) for km in [(5, 9), (6, 11)]}
+    errors = []
+
+    def work(km):
+        try:
+            k, m = km
+            codes[km].jit_prepare_encode(list(range(k, m)))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(km,)) for km in [(5, 9), (6, 11)] * 4]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    assert len(list(tmp_path.glob("zfec_hip_bitslice_k5_r4_*.co"))) == 1
+    assert len(list(tmp_path.glob("zfec_hip_bitslice_k6_r5_*.co"))) == 1
