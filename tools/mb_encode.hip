@@ -114,6 +114,18 @@ int main(int argc, char** argv) {
             printf("copy_like k=3 r=7 nt=%d                         %8.4f ms  hbm %7.1f GB/s\n", nt, ms,
                    10.0 * sz / (ms * 1e-3) / 1e9);
         }
+        {  // the encode kernel's unit walk with the GF arithmetic replaced by an XOR
+            const Variant saved = g_reg[3][7];
+            g_reg[3][7] = Variant{copy_walk<3, 7>, "copy_walk", 0, true, 1};
+            for (int gm : {2, 16}) {
+                g_grid_mult = gm;
+                MatJob jj = make_job(in, out, 3, 7, sz, sz);
+                float ms = time_ms([&] { MatJob j2 = jj; CK(launch_matapply(j2, 0)); }, 20);
+                printf("copy_walk k=3 r=7 gm=%2d                         %8.4f ms  hbm %7.1f GB/s\n", gm, ms,
+                       10.0 * sz / (ms * 1e-3) / 1e9);
+            }
+            g_reg[3][7] = saved;
+        }
         CK(hipFree(in));
         CK(hipFree(out));
     }
@@ -258,6 +270,12 @@ int main(int argc, char** argv) {
             {"reg<3,3> nt U1", matapply_reg<3, 3, true, 1>, 1, 3, 3},
             {"reg<3,3> nt U2", matapply_reg<3, 3, true, 2>, 2, 3, 3},
             {"reg<3,3> plain U1", matapply_reg<3, 3, false, 1>, 1, 3, 3},
+            {"reg<3,7> nt PF", matapply_reg<3, 7, true, 1, 0, true>, 1, 3, 7},
+            {"reg<3,7> nt W7", matapply_reg<3, 7, true, 1, 0, false, 7>, 1, 3, 7},
+            {"reg<3,7> nt W8", matapply_reg<3, 7, true, 1, 0, false, 8>, 1, 3, 7},
+            {"reg<3,7> nt PF W7", matapply_reg<3, 7, true, 1, 0, true, 7>, 1, 3, 7},
+            {"reg<3,3> nt W8", matapply_reg<3, 3, true, 1, 0, false, 8>, 1, 3, 3},
+            {"reg<3,3> nt PF", matapply_reg<3, 3, true, 1, 0, true>, 1, 3, 3},
         };
         for (auto& v : vs) {
             const Variant saved = g_reg[v.k][v.r];
@@ -269,7 +287,7 @@ int main(int argc, char** argv) {
             CK(hipMemset(xin, 0x5a, v.k * bsz));
             hipFuncAttributes attr;
             CK(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(v.fn)));
-            for (int gm : {2, 16}) {
+            for (int gm : {1, 2, 16}) {
                 g_grid_mult = gm;
                 MatJob j = make_job(xin, xout, v.k, v.r, bsz, bsz);
                 float ms = time_ms([&] { CK(launch_matapply(j, 0)); }, 20);

@@ -264,8 +264,12 @@ __device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint6
 }
 
 // U: units per lane per loop trip (U = 2 puts 2K loads in flight per lane).
-template <int K, int R, bool NT, int U = 1, int SP = 0>
-__global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
+// PF (U = 1 only): the next unit's inputs are loaded before the current unit
+// is computed, so a lane with several units (grid-stride) keeps loads in
+// flight while it computes (tools/mb_encode.hip, variants "PF").
+// W: __launch_bounds__ waves-per-SIMD floor (0: none; tools/mb_encode.hip variants "W8").
+template <int K, int R, bool NT, int U = 1, int SP = 0, bool PF = false, int W = 0>
+__global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJob job) {
     Tab T[R][K];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -275,6 +279,27 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const MatJob job) {
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
     UnitIter u(job);
+    if constexpr (PF) {
+        static_assert(U == 1, "prefetch walks one unit per trip");
+        u32x4 x[K];
+        Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
+        uint64_t ob = u.s * job.out_sstride + sp.off;
+        if (u.s < job.nstripes) reg_load<K>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
+        while (u.s < job.nstripes) {
+            UnitIter v = u;
+            v.next(job);
+            const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
+            u32x4 xn[K];
+            if (v.s < job.nstripes) reg_load<K>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
+            reg_compute_store<K, R, NT, SP>(job, T, x, ob, sp.full, sp.nb);
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = xn[j];
+            sp = spn;
+            ob = v.s * job.out_sstride + spn.off;
+            u = v;
+        }
+        return;
+    }
     while (u.s < job.nstripes) {
         uint64_t ib[U], ob[U];
         uint32_t nb[U];
@@ -604,7 +629,10 @@ int g_grid_mult = 1024;  // grid cap = CUs x resident blocks per CU x g_grid_mul
 
 template <int K, int R>
 void set_reg() {
-    g_reg[K][R] = Variant{matapply_reg<K, R, true>, kRegNames[K][R], 0, true};
+    // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
+    // tools/mb_encode.exe; no gain for the 3-row decode)
+    constexpr bool kPrefetch = R >= 5;
+    g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch>, kRegNames[K][R], 0, true};
 }
 
 template <int K>
