@@ -90,6 +90,8 @@ enum {
 #define FEC_FLAG_LIBRARY_STREAM 2u /* ignore `stream`; use the library's per-thread stream */
 #define FEC_FLAG_ALL_PRIMARIES 4u  /* decode: output all k primaries in order (present ones copied),
                                       not only the missing ones: the output is the stripe itself */
+#define FEC_FLAG_HOST_MEMORY 8u    /* every block is host memory (pageable or page-locked): skip the
+                                      per-pointer device queries (small calls from Python bytes) */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);

@@ -224,6 +224,26 @@ def test_c_abi_host_pointers():
     assert (rec == data[[0, 2, 4]]).all()
 
 
+def test_c_abi_host_memory_flag():
+    """FEC_FLAG_HOST_MEMORY (the Python bytes path): no per-pointer queries;
+    small calls through the pinned bounce buffer, large ones pinned in place."""
+    k, m = 4, 11
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(31)
+    for sz in [1, 700, 100_000, 1_500_001]:
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        out = np.zeros((m - k, sz), dtype=np.uint8)
+        code.encode_ptrs([data[i].ctypes.data for i in range(k)], [out[i].ctypes.data for i in range(m - k)],
+                         list(range(k, m)), sz, flags=capi.FEC_FLAG_LIBRARY_STREAM | capi.FEC_FLAG_HOST_MEMORY)
+        assert (out == oracle.encode(k, m, data)).all(), sz
+        slots = [7, 1, 9, 3]
+        allb = np.concatenate([data, out])
+        rec = np.zeros((2, sz), dtype=np.uint8)
+        code.decode_ptrs([allb[s].ctypes.data for s in slots], [rec[i].ctypes.data for i in range(2)], slots, sz,
+                         flags=capi.FEC_FLAG_LIBRARY_STREAM | capi.FEC_FLAG_HOST_MEMORY)
+        assert (rec == data[[0, 2]]).all(), sz
+
+
 def _encode_ptrs_check(code, k, m, data, in_addrs, out_addrs, read_out, sz):
     code.encode_ptrs(in_addrs, out_addrs, list(range(k, m)), sz, flags=0)
     got = read_out()

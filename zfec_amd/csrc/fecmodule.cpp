@@ -224,7 +224,7 @@ PyObject* Encoder_encode(Coder* self, PyObject* args) {
     int st = FEC_OK;
     if (!ids.empty()) {
         Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, in.data(), outp.data(), ids.data(), ids.size(),
-                                                  static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM);
+                                                  static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
@@ -364,7 +364,7 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
     int st = FEC_OK;
     if (!rec.empty()) {
         Py_BEGIN_ALLOW_THREADS st =
-            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM);
+            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
