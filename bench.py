@@ -253,9 +253,11 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
     for i, s in enumerate(slots):  # stage the received blocks once (not part of a step)
         recv[:, i].copy_(data[:, s] if s < k else par[:, s - k])
     dec(stream.cuda_stream)
-    # wide codes: the first launches queued background compiles of the
-    # bit-sliced kernels (zfec_amd/csrc/bitslice.cpp); wait for them so the
+    # wide codes: a matrix's second large launch queues the background compile
+    # of its bit-sliced kernel (zfec_amd/csrc/bitslice.cpp); wait for it so the
     # warmup and the timed loop run the kernels a long-running user gets
+    enc(stream.cuda_stream)
+    dec(stream.cuda_stream)
     capi.jit_wait()
     kernels = {}
     for i in range(max(1, warmup)):

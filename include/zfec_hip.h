@@ -157,9 +157,10 @@ const char* fec_last_kernel_name(void);
 
 /* Run-time specialised bit-sliced kernels (hipRTC; zfec_amd/csrc/bitslice.cpp):
  * the coefficient matrix of a launch compiled into the instruction stream.
- * mode 0 = off; 1 = auto (default; large launches of wide codes, compiled in a
- * background thread while the table kernels serve, then cached in memory and
- * in jit_cache/ next to the library); 2 = force (every launch with blocks of
+ * mode 0 = off; 1 = auto (default; launches of >= 8 MiB of wide codes: a
+ * matrix's second such launch queues its compile in a background thread while
+ * the table kernels serve; kernels are cached in memory and in jit_cache/ next
+ * to the library, at most 512); 2 = force (every launch with blocks of
  * >= 2048 bytes, compiled synchronously).  The environment variable
  * ZFEC_HIP_JIT=0|auto|force sets the initial mode.  Returns the previous
  * mode; any other value of `mode` only queries.  Results are bit-identical in

@@ -124,8 +124,9 @@ def test_jit_all_primaries_flag(force_jit):
 
 
 def test_jit_auto_policy_background_compile():
-    """Auto mode: the first large launch queues a compile and runs the table
-    kernel; after fec_jit_wait the specialised kernel runs; same bytes."""
+    """Auto mode: the second large launch of a matrix queues its compile (both
+    run the table kernel); after fec_jit_wait the specialised kernel runs;
+    same bytes."""
     prev = capi.jit_mode(capi.JIT_AUTO)
     try:
         k, m, sz = 12, 21, 4 << 20  # (k + r) * sz = 84 MiB per launch: above the auto threshold
@@ -134,10 +135,13 @@ def test_jit_auto_policy_background_compile():
         enc = zfec_amd.Encoder(k, m)
         out1 = enc.encode([data[i] for i in range(k)])
         first = capi.last_kernel_name()
+        capi.jit_wait()  # nothing queued: a matrix is compiled on its second large launch
+        enc.encode([data[i] for i in range(k)])
+        again = capi.last_kernel_name()
         capi.jit_wait()
         out2 = enc.encode([data[i] for i in range(k)])
         second = capi.last_kernel_name()
-        assert first.startswith("matapply"), first
+        assert first.startswith("matapply") and again.startswith("matapply"), (first, again)
         assert second.startswith("zfec_hip_bitslice"), (first, second)
         for a, b in zip(out1[k:], out2[k:]):
             assert bool(torch.equal(a, b))

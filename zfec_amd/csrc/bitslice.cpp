@@ -481,6 +481,7 @@ struct Registry {
     std::mutex mu;
     std::condition_variable cv;
     std::map<std::string, std::unique_ptr<Entry>> entries;
+    std::map<std::string, int> seen;  // auto mode: launches of matrices not compiled yet
     int pending = 0, ready = 0;
     std::vector<std::thread> workers;
     std::string last_error;
@@ -547,17 +548,22 @@ BsOptions options_from_env() {
 
 // Registry entry for (matrix, options); queues or runs its compile.  Called
 // with R.mu held by `lk`; releases it while compiling synchronously.
-Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
-    Registry& R = reg();
-    const BsOptions opt = options_from_env();
+std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt) {
     std::string key;
-    key.reserve(32 + size_t(k) * r);
+    key.reserve(48 + size_t(k) * r);
     char hdr[64];
     snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
              opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
-    if (opt.share && bitslice_split(r, opt)) key += "share/";
     key += hdr;
+    if (opt.share && bitslice_split(r, opt)) key += "share/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
+    return key;
+}
+
+Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
+    Registry& R = reg();
+    const BsOptions opt = options_from_env();
+    const std::string key = entry_key(coef, k, r, opt);
     auto it = R.entries.find(key);
     if (it != R.entries.end()) return it->second.get();
     auto ne = std::make_unique<Entry>();
@@ -594,8 +600,14 @@ bool eligible(const MatJob& job, JitMode mode) {
     if (mode == kJitForce) return true;
     if (job.k * job.r < 24 || (job.k <= 4 && job.r <= 8)) return false;
     const double bytes = double(job.k + job.r) * double(job.sz) * double(job.nstripes);
-    return bytes >= double(32u << 20);
+    return bytes >= double(8u << 20);
 }
+
+// Auto mode compiles a matrix on its second eligible launch (a decode with a
+// one-off erasure pattern does not queue a compile), and at most
+// kAutoMaxKernels matrices in all.
+constexpr int kAutoMinUses = 2;
+constexpr size_t kAutoMaxKernels = 512;
 
 }  // namespace
 
@@ -640,6 +652,15 @@ hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char
     if (!eligible(job, mode)) return hipErrorNotSupported;
     Registry& R = reg();
     std::unique_lock<std::mutex> lk(R.mu);
+    if (mode == kJitAuto) {
+        const std::string key = entry_key(job.coef, job.k, job.r, options_from_env());
+        if (!R.entries.count(key)) {
+            if (R.entries.size() >= kAutoMaxKernels) return hipErrorNotSupported;
+            if (R.seen.size() > 4 * kAutoMaxKernels) R.seen.clear();
+            if (++R.seen[key] < kAutoMinUses) return hipErrorNotSupported;
+            R.seen.erase(key);
+        }
+    }
     Entry* e = get_entry(job.coef, job.k, job.r, mode == kJitForce, lk);
     if (e->state == 0) {
         if (mode != kJitForce) return hipErrorNotReady;
