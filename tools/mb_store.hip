@@ -1,5 +1,6 @@
 // mb_store.hip -- cache policy of the output stores of the K=3/M=10 register
-// kernel (matapply_reg<3,7>): nt (production), sc1, sc0 sc1, nt sc1.
+// kernels (matapply_reg<3,7> encode, <3,3> decode): nt (production), sc1, sc0 sc1,
+// over K=3 single stripes of 8-512 MiB, batches of 1 MiB stripes and cfg5.
 //
 // A kernel that streams ~150 MB of stores ends with the XCD L2s full of dirty
 // lines; the end-of-kernel release writes them back before the next kernel of
@@ -33,33 +34,55 @@ int main() {
     set_jit_mode(kJitOff);
     struct V {
         const char* name;
+        int r;
         KernelFn fn;
-    } vs[] = {{"nt", matapply_reg<3, 7, true, 1, 0>},
-              {"sc1", matapply_reg<3, 7, true, 1, 1>},
-              {"sc0sc1", matapply_reg<3, 7, true, 1, 2>},
-              {"ntsc1", matapply_reg<3, 7, true, 1, 3>}};
+    } vs[] = {{"nt", 7, matapply_reg<3, 7, true, 1, 0, true>},
+              {"sc1", 7, matapply_reg<3, 7, true, 1, 1, true>},
+              {"sc0sc1", 7, matapply_reg<3, 7, true, 1, 2, true>},
+              {"dec-nt", 3, matapply_reg<3, 3, true, 1, 0>},
+              {"dec-sc0sc1", 3, matapply_reg<3, 3, true, 1, 2>}};
     const int nv = sizeof(vs) / sizeof(vs[0]);
+    // K=3 single stripes of 8 MiB .. 512 MiB, batches of 1 MiB stripes, and cfg5
     struct Shape {
-        const char* name;
+        char name[32];
         size_t sz, ld, ns;
-    } shapes[] = {{"cfg2 64MiB", 22369622, 22369792, 1}, {"1MiB x256", 349526, 349696, 256},
-                  {"cfg5 4KiB x1e6", 1366, 1536, 1000000}};
+    };
+    std::vector<Shape> shapes;
+    for (size_t mib : {8, 16, 32, 64, 96, 128, 192, 256, 512}) {
+        Shape sh;
+        snprintf(sh.name, sizeof sh.name, "%zu MiB x1", mib);
+        sh.sz = ((mib << 20) + 2) / 3;
+        sh.ld = (sh.sz + 255) / 256 * 256;
+        sh.ns = 1;
+        shapes.push_back(sh);
+    }
+    for (size_t ns : {32, 64, 128, 256}) {
+        Shape sh;
+        snprintf(sh.name, sizeof sh.name, "1 MiB x%zu", ns);
+        sh.sz = 349526;
+        sh.ld = 349696;
+        sh.ns = ns;
+        shapes.push_back(sh);
+    }
+    if (!getenv("MB_NO_CFG5")) shapes.push_back(Shape{"cfg5 4KiB x1e6", 1366, 1536, 1000000});
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     for (const Shape& sh : shapes) {
-        const int k = 3, r = 7;
+        const int k = 3, r = 7;  // buffers sized for the widest variant
         uint8_t *in, *out;
         CK(hipMalloc(&in, sh.ns * k * sh.ld));
         CK(hipMalloc(&out, sh.ns * r * sh.ld));
         CK(hipMemset(in, 0x5a, sh.ns * k * sh.ld));
         CK(hipMemset(out, 0, sh.ns * r * sh.ld));
-        std::vector<uint8_t> want, got(sh.ns * r * sh.ld);
+        // each variant's previous output is compared with the same-r variant's
+        std::vector<uint8_t> want[8], got(sh.ns * r * sh.ld);
         std::vector<std::vector<float>> t_b2b(nv), t_one(nv);
         const int reps = sh.ns > 1000 ? 5 : 20;
         for (int round = 0; round < 5; ++round)
             for (int v = 0; v < nv; ++v) {
-                Variant* slot = &g_reg[3][7];
+                const int r = vs[v].r;
+                Variant* slot = &g_reg[3][r];
                 const Variant saved = *slot;
                 *slot = Variant{vs[v].fn, vs[v].name, 0, true, 1};
                 MatJob j;
@@ -81,9 +104,9 @@ int main() {
                 CK(hipDeviceSynchronize());
                 if (round == 0) {
                     CK(hipMemcpy(got.data(), out, got.size(), hipMemcpyDeviceToHost));
-                    if (want.empty())
-                        want = got;
-                    else if (memcmp(want.data(), got.data(), got.size()))
+                    if (want[r].empty())
+                        want[r] = got;
+                    else if (memcmp(want[r].data(), got.data(), got.size()))
                         printf("MISMATCH %s %s\n", sh.name, vs[v].name);
                 }
                 CK(hipEventRecord(a, 0));
@@ -109,8 +132,8 @@ int main() {
         for (int v = 0; v < nv; ++v) {
             std::sort(t_b2b[v].begin(), t_b2b[v].end());
             std::sort(t_one[v].begin(), t_one[v].end());
-            const double bytes = double(k + r) * sh.sz * sh.ns;
-            printf("%-16s %-7s back-to-back %8.4f ms (%6.1f GB/s)   single %8.4f ms (%6.1f GB/s)\n", sh.name, vs[v].name,
+            const double bytes = double(k + vs[v].r) * sh.sz * sh.ns;
+            printf("%-16s %-10s back-to-back %8.4f ms (%6.1f GB/s)   single %8.4f ms (%6.1f GB/s)\n", sh.name, vs[v].name,
                    t_b2b[v][2], bytes / (t_b2b[v][2] * 1e-3) / 1e9, t_one[v][2], bytes / (t_one[v][2] * 1e-3) / 1e9);
         }
         CK(hipFree(in));
