@@ -162,6 +162,16 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     else
         e("extern \"C\" __global__ __launch_bounds__(%u) void %s(const Args a) {\n", threads, name);
     e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n");
+    // argload: block pointers are read from the kernel-argument segment where
+    // they are used, through a pointer the compiler must treat as new in every
+    // scope (empty asm), instead of all being loaded up front and spilled
+    const char* const PA = opt.argload ? "ka->" : "a.";
+    if (opt.argload)
+        e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
+          "  const KArgs ka0 = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();\n");
+    auto launder = [&](const char* indent) {
+        if (opt.argload) e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
+    };
     if (split && opt.share) {
         e("  __shared__ u32x4 sh[%u];  // [input][half][lane] bit-planes of the unit\n", k * 128);
         e("  const u32 lane = threadIdx.x & 63u;\n");
@@ -178,6 +188,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     e("    if (off > a.sz - %uu) off = a.sz - %uu;  // the last chunk ends at sz (overlapping its neighbour)\n",
       kBsChunk, kBsChunk);
     e("    const u64 ub = (u64)s * a.iss + off, uo = (u64)s * a.oss + off;\n");
+    if (!split) launder("    ");
 
     // Steps: (tile t, input j) in order; loads run `prefetch` steps ahead
     // (across tiles, or inside each tile when split).
@@ -192,7 +203,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, j * 128, n, j * 128 + 64);
             return;
         }
-        e("    const __amdgpu_buffer_rsrc_t ri%u = rs(a.in[%u] + ub);\n", n, j);
+        e("    const __amdgpu_buffer_rsrc_t ri%u = rs(%sin[%u] + ub);\n", n, PA, j);
         e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", n, n, n, n);
     };
     if (!split)
@@ -202,8 +213,9 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         for (unsigned t = 0; t < ntiles; ++t) {
             if (t >= k) break;
             e("    if (tile == %uu) {\n", t);
+            launder("      ");
             for (unsigned j = t; j < k; j += ntiles) {
-                e("      const __amdgpu_buffer_rsrc_t pi%u = rs(a.in[%u] + ub);\n", j, j);
+                e("      const __amdgpu_buffer_rsrc_t pi%u = rs(%sin[%u] + ub);\n", j, PA, j);
                 e("      const u32x4 p%u_0 = ld(pi%u, lo16), p%u_1 = ld(pi%u, lo16 + 1024u);\n", j, j, j, j);
             }
             for (unsigned j = t; j < k; j += ntiles) {
@@ -225,6 +237,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         e("    // tile %u: rows %u..%u\n", t, r0, r1 - 1);
         if (split) {
             e("    if (tile == %uu) {\n", t);
+            launder("    ");
             for (unsigned n = t * k; n < t * k + pf && n < seq_end; ++n) emit_load(n);
         }
         std::vector<char> init(size_t(r1 - r0) * 8, 0);
@@ -305,7 +318,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             for (unsigned b = 0; b < 8; ++b)
                 if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
             e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
-            e("    const __amdgpu_buffer_rsrc_t ro%u = rs(a.out[%u] + uo);\n", i, i);
+            e("    const __amdgpu_buffer_rsrc_t ro%u = rs(%sout[%u] + uo);\n", i, PA, i);
             e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
             e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
         }
@@ -542,6 +555,7 @@ BsOptions options_from_env() {
     o.waves = env_uint("ZFEC_HIP_JIT_WAVES", o.waves);
     o.split = env_uint("ZFEC_HIP_JIT_SPLIT", o.split ? 1 : 0) != 0;
     o.share = env_uint("ZFEC_HIP_JIT_SHARE", o.share ? 1 : 0) != 0;
+    o.argload = env_uint("ZFEC_HIP_JIT_ARGLOAD", o.argload ? 1 : 0) != 0;
     if (o.waves > 8) o.waves = 8;
     return o;
 }
@@ -555,6 +569,7 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
              opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
     key += hdr;
+    if (opt.argload) key += "argload/";
     if (opt.share && bitslice_split(r, opt)) key += "share/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;

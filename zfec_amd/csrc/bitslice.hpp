@@ -37,6 +37,7 @@ struct BsOptions {
     unsigned waves = 0;              // __launch_bounds__ waves-per-SIMD hint (0: none)
     bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
     bool share = true;               // split: inputs transposed once per unit, bit-planes shared through LDS
+    bool argload = true;             // block pointers loaded where used (no up-front SGPR spill)
 };
 
 // Row tiles of an r-row matrix, and whether they go to the waves of one
