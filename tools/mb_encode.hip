@@ -276,6 +276,9 @@ int main(int argc, char** argv) {
             {"reg<3,7> nt PF W7", matapply_reg<3, 7, true, 1, 0, true, 7>, 1, 3, 7},
             {"reg<3,3> nt W8", matapply_reg<3, 3, true, 1, 0, false, 8>, 1, 3, 3},
             {"reg<3,3> nt PF", matapply_reg<3, 3, true, 1, 0, true>, 1, 3, 3},
+            {"reg<3,7> nt PF AL", matapply_reg<3, 7, true, 1, 0, true, 0, true>, 1, 3, 7},
+            {"reg<3,7> nt U1 AL", matapply_reg<3, 7, true, 1, 0, false, 0, true>, 1, 3, 7},
+            {"reg<3,3> nt U1 AL", matapply_reg<3, 3, true, 1, 0, false, 0, true>, 1, 3, 3},
         };
         for (auto& v : vs) {
             const Variant saved = g_reg[v.k][v.r];

@@ -229,8 +229,21 @@ __device__ __forceinline__ Span chunk_span(uint32_t c, uint64_t sz, uint32_t nfu
 // kernel arguments (prefetched scalar loads); the compiler keeps the high
 // words in SGPRs and copies the low words to VGPRs once, outside the loop.
 // ---------------------------------------------------------------------------
-// One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.
-template <int K, int R, bool NT, int SP = 0>
+// The kernel's MatJob argument read in place from the kernel-argument segment
+// through a pointer the compiler must treat as new at every call (empty asm):
+// the loads stay where they are used instead of all being hoisted into the
+// prologue, where the 5*K*R table dwords and the block pointers overflow the
+// SGPRs and spill to VGPR lanes (v_writelane / v_readlane per wave).
+typedef const __attribute__((address_space(4))) MatJob* KJob;
+__device__ __forceinline__ KJob kernarg_job() {
+    KJob kj = (KJob)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kj));
+    return kj;
+}
+
+// One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.  AL: each
+// row's tables and output pointer are loaded (scalar loads) right before use.
+template <int K, int R, bool NT, int SP = 0, bool AL = false>
 __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
                                                   uint64_t ob, bool full, uint32_t nb) {
     Sel sel[4][K];
@@ -243,12 +256,26 @@ __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const u32x4 y{gf_dot<K>(T[r], sel[0]), gf_dot<K>(T[r], sel[1]), gf_dot<K>(T[r], sel[2]),
-                      gf_dot<K>(T[r], sel[3])};
+        Tab t[K];
+        uint8_t* out;
+        if constexpr (AL) {
+            const KJob kj = kernarg_job();
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t i = (r * K + j) * 5;
+                t[j] = Tab{kj->tab[i], kj->tab[i + 1], kj->tab[i + 2], kj->tab[i + 3], kj->tab[i + 4]};
+            }
+            out = kj->out[r];
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) t[j] = T[r][j];
+            out = job.out[r];
+        }
+        const u32x4 y{gf_dot<K>(t, sel[0]), gf_dot<K>(t, sel[1]), gf_dot<K>(t, sel[2]), gf_dot<K>(t, sel[3])};
         if (full)
-            store16_pol<NT, SP>(job.out[r] + ob, y);
+            store16_pol<NT, SP>(out + ob, y);
         else
-            store_tail(job.out[r] + ob, y, nb);
+            store_tail(out + ob, y, nb);
     }
 }
 
@@ -268,13 +295,16 @@ __device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint6
 // is computed, so a lane with several units (grid-stride) keeps loads in
 // flight while it computes (tools/mb_encode.hip, variants "PF").
 // W: __launch_bounds__ waves-per-SIMD floor (0: none; tools/mb_encode.hip variants "W8").
-template <int K, int R, bool NT, int U = 1, int SP = 0, bool PF = false, int W = 0>
+// AL: tables and output pointers read where they are used (reg_compute_store).
+template <int K, int R, bool NT, int U = 1, int SP = 0, bool PF = false, int W = 0, bool AL = false>
 __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJob job) {
     Tab T[R][K];
+    if constexpr (!AL) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int j = 0; j < K; ++j) T[r][j] = karg_table(job, r * K + j);
+            for (int j = 0; j < K; ++j) T[r][j] = karg_table(job, r * K + j);
+    }
 
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
@@ -291,7 +321,7 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
             const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
             u32x4 xn[K];
             if (v.s < job.nstripes) reg_load<K>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
-            reg_compute_store<K, R, NT, SP>(job, T, x, ob, sp.full, sp.nb);
+            reg_compute_store<K, R, NT, SP, AL>(job, T, x, ob, sp.full, sp.nb);
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = xn[j];
             sp = spn;
@@ -318,7 +348,7 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
         }
 #pragma unroll
         for (int i = 0; i < U; ++i)
-            if (live[i]) reg_compute_store<K, R, NT, SP>(job, T, x[i], ob[i], full[i], nb[i]);
+            if (live[i]) reg_compute_store<K, R, NT, SP, AL>(job, T, x[i], ob[i], full[i], nb[i]);
     }
 }
 
@@ -632,7 +662,11 @@ void set_reg() {
     // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
     // tools/mb_encode.exe; no gain for the 3-row decode)
     constexpr bool kPrefetch = R >= 5;
-    g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch>, kRegNames[K][R], 0, true};
+    // more table dwords than the SGPRs hold next to the pointers: read them
+    // where they are used (K=3/M=10 encode 35.9 -> 33.6 us, tools/mb_encode.exe
+    // variant "PF AL"; the 3-row decode is unchanged either way)
+    constexpr bool kArgLoad = K * R * 5 > 60;
+    g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch, 0, kArgLoad>, kRegNames[K][R], 0, true};
 }
 
 template <int K>
