@@ -665,7 +665,7 @@ void set_reg() {
     // more table dwords than the SGPRs hold next to the pointers: read them
     // where they are used (K=3/M=10 encode 35.9 -> 33.6 us, tools/mb_encode.exe
     // variant "PF AL"; the 3-row decode is unchanged either way)
-    constexpr bool kArgLoad = K * R * 5 > 60;
+    constexpr bool kArgLoad = K * R * 5 >= 50;
     g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch, 0, kArgLoad>, kRegNames[K][R], 0, true};
 }
 
