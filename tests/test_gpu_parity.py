@@ -420,6 +420,47 @@ def test_config2_64mib_vs_oracle():
     assert (torch.stack(dec).cpu().numpy() == data).all()
 
 
+def _batched_full_size(k, m, S, ns, seed, sample):
+    """BASELINE batched configs at full size: one encode launch over all
+    stripes ([stripe][block][row] rows 256-byte aligned, as bench.py lays them
+    out), a decode from the last k blocks; the decode must return every
+    stripe (device-side equality), and sampled stripes' parity must equal
+    the oracle's."""
+    r = m - k
+    sz = -(-S // k)
+    ld = -(-sz // 256) * 256
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=g)
+    par = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns, stream=st)
+    slots = place(list(range(m - k, m)), k)
+    recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
+    for i, s in enumerate(slots):
+        recv[:, i].copy_(data[:, s] if s < k else par[:, s - k])
+    missing = [i for i in range(k) if slots[i] >= k]
+    rec = torch.zeros((ns, len(missing), ld), dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, len(missing) * ld, slots, sz, ns, stream=st)
+    torch.cuda.synchronize()
+    assert bool(torch.equal(rec[:, :, :sz], data[:, missing, :sz]))
+    assert int(par[:, :, sz:].count_nonzero()) == 0  # nothing written past the block ends
+    rng = np.random.default_rng(seed)
+    for s in sorted(set(int(x) for x in rng.integers(0, ns, size=sample))) + [0, ns - 1]:
+        got = par[s, :, :sz].cpu().numpy()
+        assert (got == oracle.encode(k, m, data[s, :, :sz].cpu().numpy())).all(), s
+
+
+def test_config4_1024_stripes_of_1mib():
+    """cfg4: K=20/M=60, 1024 x 1 MiB stripes in one launch."""
+    _batched_full_size(20, 60, 1 << 20, 1024, 4, sample=6)
+
+
+def test_config5_1e6_objects_of_4kib():
+    """cfg5: K=3/M=10, 10^6 x 4 KiB objects (1366-byte blocks) in one launch."""
+    _batched_full_size(3, 10, 4096, 10 ** 6, 5, sample=200)
+
+
 def test_config3_256mib_roundtrip():
     """K=10/M=16, 256 MiB: encode, drop primaries 0-5, decode; compare by
     equality on the device (size-independent property) and spot-check parity
