@@ -82,8 +82,15 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # ZFEC_BENCH_BACKEND=gloo rehearses the multi-rank path with several
+        # ranks on one GPU (the driver's runs use RCCL, one rank per GPU)
+        backend = os.environ.get("ZFEC_BENCH_BACKEND", "nccl")
+        if backend == "gloo":
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return dist, rank, world
     torch.cuda.set_device(0)
     return None, 0, 1
@@ -97,7 +104,7 @@ def barrier(dist):
 def reduce(dist, x, op):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if dist.get_backend() == "gloo" else "cuda")
     dist.all_reduce(t, op=op)
     return float(t.item())
 
