@@ -126,6 +126,18 @@ int main(int argc, char** argv) {
             }
             g_reg[3][7] = saved;
         }
+        {  // the same for the decode shape (3 inputs, 3 outputs)
+            const Variant saved = g_reg[3][3];
+            g_reg[3][3] = Variant{copy_walk<3, 3>, "copy_walk", 0, true, 1};
+            for (int gm : {2, 16}) {
+                g_grid_mult = gm;
+                MatJob jj = make_job(in, out, 3, 3, sz, sz);
+                float ms = time_ms([&] { MatJob j2 = jj; CK(launch_matapply(j2, 0)); }, 20);
+                printf("copy_walk k=3 r=3 gm=%2d                         %8.4f ms  hbm %7.1f GB/s\n", gm, ms,
+                       6.0 * sz / (ms * 1e-3) / 1e9);
+            }
+            g_reg[3][3] = saved;
+        }
         CK(hipFree(in));
         CK(hipFree(out));
     }
@@ -279,6 +291,8 @@ int main(int argc, char** argv) {
             {"reg<3,7> nt PF AL", matapply_reg<3, 7, true, 1, 0, true, 0, true>, 1, 3, 7},
             {"reg<3,7> nt U1 AL", matapply_reg<3, 7, true, 1, 0, false, 0, true>, 1, 3, 7},
             {"reg<3,3> nt U1 AL", matapply_reg<3, 3, true, 1, 0, false, 0, true>, 1, 3, 3},
+            {"reg<3,3> nt PF AL", matapply_reg<3, 3, true, 1, 0, true, 0, true>, 1, 3, 3},
+            {"reg<3,3> nt U2 AL", matapply_reg<3, 3, true, 2, 0, false, 0, true>, 2, 3, 3},
         };
         for (auto& v : vs) {
             const Variant saved = g_reg[v.k][v.r];
