@@ -161,12 +161,9 @@ int ensure_hbuf(DevCtx& d, size_t bytes) {
     return FEC_OK;
 }
 
-// Device id of a device-accessible allocation, or -1 for host memory; *pinned
-// tells page-locked host memory (hipHostMalloc / hipHostRegister, torch
-// pin_memory) -- DMA-able in place -- from pageable memory.
 // Device holding p, or -1 for host memory.  For page-locked host memory
-// (hipHostMalloc / hipHostRegister) *pinned is set and *dev_ptr is the address
-// a kernel uses to read / write it over PCIe.
+// (hipHostMalloc / hipHostRegister, torch pin_memory) *pinned is set and
+// *dev_ptr is the address a kernel uses to read / write it over PCIe.
 int pointer_device(const void* p, bool* pinned = nullptr, void** dev_ptr = nullptr) {
     hipPointerAttribute_t a;
     if (pinned) *pinned = false;
