@@ -170,10 +170,10 @@ int main(int argc, char** argv) {
             const char* name;
             KernelFn fn;
             int upl;
-        } vs[] = {{"reg<3,7>", matapply_reg<3, 7, true, 1>, 1}, {"copy_walk", copy_walk<3, 7>, 1},
+        } vs[] = {{"reg<3,7>PF-AL", matapply_reg<3, 7, true, 1, 0, true, 0, true>, 1}, {"copy_walk", copy_walk<3, 7>, 1},
                   {"reg<3,7>U2", matapply_reg<3, 7, true, 2>, 2}};
         std::vector<std::vector<float>> t(3 * 4);
-        const int gms[4] = {4, 16, 64, 1024};
+        const int gms[4] = {16, 64, 256, 1024};
         for (int round = 0; round < 5; ++round)
             for (int i = 0; i < 3; ++i)
                 for (int g = 0; g < 4; ++g) {
