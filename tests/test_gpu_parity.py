@@ -355,6 +355,25 @@ def test_torch_tensors_roundtrip():
         assert (torch.stack(dec).cpu().numpy() == data).all()
 
 
+def test_torch_tensor_preconditions():
+    """Device blocks: non-contiguous, mixed host/device, different lengths -> Error."""
+    t = torch.zeros((4, 8), dtype=torch.uint8, device="cuda")
+    enc = zfec_amd.Encoder(2, 4)
+    with pytest.raises(zfec_amd.Error, match="C-contiguous"):
+        enc.encode([t[:, 0], t[:, 1]])
+    with pytest.raises(zfec_amd.Error, match="all device tensors"):
+        enc.encode([t[0], b"\x00" * 8])
+    with pytest.raises(zfec_amd.Error, match="same length"):
+        enc.encode([t[0], t[1, :4]])
+    with pytest.raises(zfec_amd.Error, match="distinct"):
+        zfec_amd.Decoder(2, 4).decode([t[0], t[1]], [3, 3])
+    # non-uint8 tensors are encoded as their bytes
+    f = torch.arange(8, dtype=torch.float32, device="cuda").reshape(2, 4)
+    out = enc.encode([f[0], f[1]])
+    ref = zfec_amd.Encoder(2, 4).encode([f[0].cpu().numpy().tobytes(), f[1].cpu().numpy().tobytes()])
+    assert [bytes(o.cpu().numpy().tobytes()) for o in out[2:]] == ref[2:]
+
+
 # ---- batched entry points -------------------------------------------------------
 
 @pytest.mark.parametrize("k,m,sz,ns", [(3, 10, 1366, 2000), (20, 60, 52429, 8), (10, 16, 100, 33), (3, 10, 16, 5)])

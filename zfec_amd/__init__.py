@@ -44,6 +44,9 @@ def _stream_handle(device):
 
 
 def _device_blocks(blocks, k):
+    for b in blocks:
+        if not _is_device_tensor(b):
+            raise Error("Precondition violation: blocks are required to be all device tensors or all host buffers")
     bl = [_byte_view(b) for b in blocks]
     if len(bl) != k:
         raise Error(
