@@ -146,6 +146,43 @@ def pmc_traffic(workload):
         return None
 
 
+# VALU issue ceiling: 256 CUs x 4 SIMDs x ~2.4 GHz / 4.25 cycles per VOP3 wave-instruction
+# (the measured v_perm_b32 / v_bitop3_b32 rate, tools/mb_valu.hip)
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4.25
+
+
+def _same_kernel(traced, printed):
+    """rocprof's demangled template name vs the library's short variant name."""
+    if traced == printed:
+        return True
+    if "<" not in traced or "<" not in printed or traced.split("<")[0] != printed.split("<")[0]:
+        return False
+    nums = [a.strip() for a in traced.split("<", 1)[1].rstrip(">").split(",") if a.strip().isdigit()]
+    pargs = [a.strip() for a in printed.split("<", 1)[1].rstrip(">").split(",") if a.strip().isdigit()]
+    return nums[:len(pargs)] == pargs
+
+
+def valu_roofline(workload, kernel, launch_ms):
+    """Second roofline of the dominant kernel: VALU wave-instructions per launch
+    (SQ_INSTS_VALU from the committed counter summary, tools/pmc_sq.sh) over the
+    launch duration, against the VALU issue ceiling."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_sq_summary.json")) as f:
+            d = json.load(f)["workloads"].get(workload, {})
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, c in d.items():
+        if _same_kernel(name, kernel) and c.get("SQ_INSTS_VALU"):
+            n = float(c["SQ_INSTS_VALU"])
+            ach = n / (launch_ms * 1e-3)
+            return {"bound": "valu-issue", "insts_per_launch": int(n), "achieved": round(ach / 1e9, 1),
+                    "peak": round(VALU_PEAK_INSTS / 1e9, 1), "unit": "G VALU wave-instructions/s",
+                    "frac": round(ach / VALU_PEAK_INSTS, 4),
+                    "basis": "SQ_INSTS_VALU per dispatch (profiles/pmc_sq_summary.json) / launch_ms; peak = "
+                             "1024 SIMDs x 2.4 GHz / 4.25 cycles per VOP3 wave-instruction (measured)"}
+    return None
+
+
 def cpu_baseline(seconds, k, m, sz):
     """Bounded CPU sample of the same workload (encode + last-k decode
     of one stripe of k*sz bytes per step, decoding from the last k blocks), one
@@ -449,6 +486,7 @@ def main():
                             "kernel": "%s (decode)" % t["kernels"]["decode"],
                             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4),
                             "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4)},
+        "valu_roofline": valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
         "encode_input_GBps": round(k * sz * ns / (t["enc_ms"] * 1e-3) / 1e9, 1),
