@@ -32,10 +32,10 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
 VARIANTS = [
     ("table", capi.JIT_OFF, {}),
-    ("split", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "0"}),
     ("share", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1"}),
-    ("share_noargload", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_ARGLOAD": "0"}),
-    ("share_t8", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_TILE": "8"}),
+    ("share_pf1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "1"}),
+    ("share_pf1_w4", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "1", "ZFEC_HIP_JIT_WAVES": "4"}),
+    ("share_pf0_w4", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "0", "ZFEC_HIP_JIT_WAVES": "4"}),
 ]
 KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE",
          "ZFEC_HIP_JIT_ORDER", "ZFEC_HIP_JIT_WAVES", "ZFEC_HIP_JIT_SPLIT", "ZFEC_HIP_JIT_SHARE",
