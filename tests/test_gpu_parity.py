@@ -402,6 +402,44 @@ def test_batch_encode_decode(k, m, sz, ns):
     assert (rec.cpu().numpy() == data[:, missing, :]).all()
 
 
+@pytest.mark.parametrize("k,m,sz,ns,rows", [(3, 10, 1366, 300, True), (2, 10, 1025, 64, True), (4, 12, 4096, 100, True),
+                                            (1, 9, 2049, 80, True), (3, 10, 1024, 100, False), (3, 10, 4097, 70, False),
+                                            (3, 10, 1366, 63, False)])
+def test_batch_short_rows_walk(k, m, sz, ns, rows):
+    """Short blocks of many stripes go through the one-wave-per-stripe walk
+    (matapply_rows, 1 KiB < sz <= 4 KiB, >= 64 stripes): every stripe against
+    the oracle, rows at an odd stride with guard bytes that must stay zero."""
+    r = m - k
+    ld = sz + 40
+    rng = np.random.default_rng(sz * 7 + ns)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    host = np.zeros((ns, k, ld), dtype=np.uint8)
+    host[:, :, :sz] = data
+    src = torch.from_numpy(host).cuda()
+    dst = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns, stream=st)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name().startswith("matapply_rows" if rows else "matapply_reg"), capi.last_kernel_name()
+    out = dst.cpu().numpy()
+    assert out[:, :, sz:].sum() == 0
+    for s in range(ns):
+        assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s
+    slots = place(list(range(m - k, m)), k)
+    allb = np.concatenate([data, out[:, :, :sz]], axis=1)
+    recv = np.zeros((ns, k, ld), dtype=np.uint8)
+    recv[:, :, :sz] = allb[:, slots, :]
+    missing = [i for i in range(k) if slots[i] >= k]
+    rec = torch.zeros((ns, len(missing), ld), dtype=torch.uint8, device="cuda")
+    code.decode_batch(torch.from_numpy(recv).cuda().data_ptr(), ld, k * ld, rec.data_ptr(), ld, len(missing) * ld,
+                      slots, sz, ns, stream=st)
+    torch.cuda.synchronize()
+    rv = rec.cpu().numpy()
+    assert (rv[:, :, :sz] == data[:, missing, :]).all()
+    assert rv[:, :, sz:].sum() == 0
+
+
 @pytest.mark.parametrize("k,m,nums", [(3, 10, [7, 1, 9]), (5, 9, [0, 1, 2, 3, 4]), (10, 16, list(range(6, 16)))])
 def test_decode_all_primaries_flag(k, m, nums):
     """FEC_FLAG_ALL_PRIMARIES: the k outputs are the primaries in order, present ones copied."""
