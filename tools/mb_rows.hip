@@ -86,6 +86,44 @@ __global__ __launch_bounds__(256) void row_walk(const MatJob job) {
     }
 }
 
+// variants of the row walk: MODE 1 = 32 bytes per lane (bytes 32l and 32l + 16),
+// MODE 2 = two stripes per wave (half-wave per stripe, 16 bytes at 16l' + 512h)
+template <int K, int R, bool GF, int MODE>
+__global__ __launch_bounds__(256) void row_walk2(const MatJob job) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t sz = job.sz;
+    Tab T[R][K];
+    auto unit = [&](uint64_t s, uint64_t off) {
+        const uint64_t o = off + 16u <= sz ? off : sz - 16u;
+        const uint64_t ib = s * job.in_sstride + o, ob = s * job.out_sstride + o;
+        u32x4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + ib);
+        if constexpr (GF) {
+            reg_compute_store<K, R, true, 0, true>(job, T, x, ob, true, 16u);
+        } else {
+            u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < K; ++j) acc ^= x[j];
+#pragma unroll
+            for (int r = 0; r < R; ++r) store16_out<true>(job.out[r] + ob, acc ^ uint32_t(r));
+        }
+    };
+    if constexpr (MODE == 1) {
+        const uint32_t nw = gridDim.x * 4u;
+        for (uint32_t s = blockIdx.x * 4u + (threadIdx.x >> 6); s < job.nstripes; s += nw)
+            for (uint64_t off = lane * 32u; off < sz; off += 2048u) {
+                unit(s, off);
+                if (off + 16u < sz) unit(s, off + 16u);
+            }
+    } else {
+        const uint32_t nw = gridDim.x * 8u;
+        const uint32_t l = lane & 31u;
+        for (uint32_t s = blockIdx.x * 8u + (threadIdx.x >> 5); s < job.nstripes; s += nw)
+            for (uint64_t off = l * 16u; off < sz; off += 512u) unit(s, off);
+    }
+}
+
 }  // namespace
 
 int main() {
@@ -128,14 +166,18 @@ int main() {
         const uint32_t g_full = uint32_t((ns + 3) / 4), g_cap = uint32_t(256 * std::max(nb, 1) * 16);
         struct V {
             const char* name;
-            int kind;  // 0 production, 1 unit copy, 2 row copy, 3 row GF
+            int kind;  // 0 production, 1 unit copy, 2 row copy, 3 row GF, 4-7 row_walk2 copy / GF
             uint32_t grid;
         } vs[] = {{"production reg<3,7>", 0, 0},
                   {"unit-walk copy", 1, 0},
                   {"row-walk copy, 1 stripe/wave", 2, g_full},
                   {"row-walk copy, 16x resident", 2, std::min(g_full, g_cap)},
                   {"row-walk GF, 1 stripe/wave", 3, g_full},
-                  {"row-walk GF, 16x resident", 3, std::min(g_full, g_cap)}};
+                  {"row-walk GF, 16x resident", 3, std::min(g_full, g_cap)},
+                  {"row-walk 32B/lane copy", 4, g_full},
+                  {"row-walk 32B/lane GF", 5, g_full},
+                  {"row-walk 2 stripes/wave copy", 6, uint32_t((ns + 7) / 8)},
+                  {"row-walk 2 stripes/wave GF", 7, uint32_t((ns + 7) / 8)}};
         const int nv = sizeof(vs) / sizeof(vs[0]);
         std::vector<std::vector<float>> t(nv);
         std::vector<uint8_t> ref, got(size_t(2000) * r * ld);
@@ -155,14 +197,22 @@ int main() {
                         hipLaunchKernelGGL((unit_copy<3, 7>), dim3(grid), dim3(256), 0, 0, jj);
                     } else if (vs[v].kind == 2) {
                         hipLaunchKernelGGL((row_walk<3, 7, false>), dim3(vs[v].grid), dim3(256), 0, 0, j);
-                    } else {
+                    } else if (vs[v].kind == 3) {
                         hipLaunchKernelGGL((row_walk<3, 7, true>), dim3(vs[v].grid), dim3(256), 0, 0, jt);
+                    } else if (vs[v].kind == 4) {
+                        hipLaunchKernelGGL((row_walk2<3, 7, false, 1>), dim3(vs[v].grid), dim3(256), 0, 0, j);
+                    } else if (vs[v].kind == 5) {
+                        hipLaunchKernelGGL((row_walk2<3, 7, true, 1>), dim3(vs[v].grid), dim3(256), 0, 0, jt);
+                    } else if (vs[v].kind == 6) {
+                        hipLaunchKernelGGL((row_walk2<3, 7, false, 2>), dim3(vs[v].grid), dim3(256), 0, 0, j);
+                    } else {
+                        hipLaunchKernelGGL((row_walk2<3, 7, true, 2>), dim3(vs[v].grid), dim3(256), 0, 0, jt);
                     }
                 };
                 launch();
                 launch();
                 CK(hipDeviceSynchronize());
-                if (round == 0 && (vs[v].kind == 0 || vs[v].kind == 3)) {  // GF variants agree on 2000 stripes
+                if (round == 0 && (vs[v].kind == 0 || vs[v].kind == 3 || vs[v].kind == 5 || vs[v].kind == 7)) {
                     CK(hipMemcpy(got.data(), out, got.size(), hipMemcpyDeviceToHost));
                     if (vs[v].kind == 0)
                         ref = got;
