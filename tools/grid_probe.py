@@ -17,11 +17,11 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = [
     (3, 10, 1366, 10 ** 6, 1536),
     (3, 10, 1366, 10 ** 6, 1408),
-    (3, 10, 22369622, 1, 22369792),
-    (3, 10, 349526, 256, 349696),
-    (10, 16, 410, 10 ** 6, 512),
-    (10, 16, 410, 10 ** 6, 640),
-    (20, 60, 52429, 1024, 52480),
+    (3, 10, 1366, 10 ** 6, 1664),
+    (3, 10, 2730, 5 * 10 ** 5, 2816),
+    (3, 10, 2730, 5 * 10 ** 5, 2944),
+    (4, 12, 4096, 3 * 10 ** 5, 4096),
+    (4, 12, 4096, 3 * 10 ** 5, 4224),
 ]
 
 
@@ -52,7 +52,7 @@ def timed(fn, n=10):
 def main():
     capi.jit_mode(capi.JIT_OFF)
     st = torch.cuda.current_stream().cuda_stream
-    gm = os.environ.get("ZFEC_HIP_GRID_MULT", "default")
+    gm = os.environ.get("ZFEC_HIP_ROWS_MULT", "default")
     for k, m, sz, ns, ld in SHAPES:
         r = m - k
         code = capi.Code(k, m)

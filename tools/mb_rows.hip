@@ -86,6 +86,24 @@ __global__ __launch_bounds__(256) void row_walk(const MatJob job) {
     }
 }
 
+// row walk over a contiguous range of stripes per wave (grid below one wave per stripe)
+template <int K, int R>
+__global__ __launch_bounds__(256) void row_walk_chunked(const MatJob job) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint64_t sz = job.sz;
+    const uint32_t per = (job.nstripes + nw - 1) / nw;
+    const uint32_t s0 = w * per, s1 = min(job.nstripes, s0 + per);
+    Tab T[R][K];
+    for (uint32_t s = s0; s < s1; ++s)
+        for (uint64_t off = lane * 16u; off < sz; off += 1024u) {
+            const uint64_t o = off + 16u <= sz ? off : sz - 16u;
+            u32x4 x[K];
+            reg_load<K>(job, x, s * job.in_sstride + o, true, 16u);
+            reg_compute_store<K, R, true, 0, true>(job, T, x, s * job.out_sstride + o, true, 16u);
+        }
+}
+
 // variants of the row walk: MODE 1 = 32 bytes per lane (bytes 32l and 32l + 16),
 // MODE 2 = two stripes per wave (half-wave per stripe, 16 bytes at 16l' + 512h)
 template <int K, int R, bool GF, int MODE>
@@ -134,7 +152,7 @@ int main() {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (size_t ld : {size_t(1536), size_t(1408)}) {
+    for (size_t ld : {size_t(1536), size_t(1408), size_t(1366), size_t(1664)}) {
         uint8_t *in, *out;
         CK(hipMalloc(&in, ns * k * ld));
         CK(hipMalloc(&out, ns * r * ld));
@@ -174,10 +192,10 @@ int main() {
                   {"row-walk copy, 16x resident", 2, std::min(g_full, g_cap)},
                   {"row-walk GF, 1 stripe/wave", 3, g_full},
                   {"row-walk GF, 16x resident", 3, std::min(g_full, g_cap)},
-                  {"row-walk 32B/lane copy", 4, g_full},
-                  {"row-walk 32B/lane GF", 5, g_full},
-                  {"row-walk 2 stripes/wave copy", 6, uint32_t((ns + 7) / 8)},
-                  {"row-walk 2 stripes/wave GF", 7, uint32_t((ns + 7) / 8)}};
+                  {"row-walk GF, 4x resident", 3, std::min(g_full, g_cap / 4)},
+                  {"row-walk GF, 64x resident", 3, std::min(g_full, g_cap * 4)},
+                  {"row-walk GF chunked, 16x res", 8, std::min(g_full, g_cap)},
+                  {"row-walk GF chunked, 4x res", 8, std::min(g_full, g_cap / 4)}};
         const int nv = sizeof(vs) / sizeof(vs[0]);
         std::vector<std::vector<float>> t(nv);
         std::vector<uint8_t> ref, got(size_t(2000) * r * ld);
@@ -199,6 +217,8 @@ int main() {
                         hipLaunchKernelGGL((row_walk<3, 7, false>), dim3(vs[v].grid), dim3(256), 0, 0, j);
                     } else if (vs[v].kind == 3) {
                         hipLaunchKernelGGL((row_walk<3, 7, true>), dim3(vs[v].grid), dim3(256), 0, 0, jt);
+                    } else if (vs[v].kind == 8) {
+                        hipLaunchKernelGGL((row_walk_chunked<3, 7>), dim3(vs[v].grid), dim3(256), 0, 0, jt);
                     } else if (vs[v].kind == 4) {
                         hipLaunchKernelGGL((row_walk2<3, 7, false, 1>), dim3(vs[v].grid), dim3(256), 0, 0, j);
                     } else if (vs[v].kind == 5) {
@@ -212,7 +232,8 @@ int main() {
                 launch();
                 launch();
                 CK(hipDeviceSynchronize());
-                if (round == 0 && (vs[v].kind == 0 || vs[v].kind == 3 || vs[v].kind == 5 || vs[v].kind == 7)) {
+                if (round == 0 && (vs[v].kind == 0 || vs[v].kind == 3 || vs[v].kind == 5 || vs[v].kind == 7 ||
+                                   vs[v].kind == 8)) {
                     CK(hipMemcpy(got.data(), out, got.size(), hipMemcpyDeviceToHost));
                     if (vs[v].kind == 0)
                         ref = got;
