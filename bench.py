@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--no-extra", action="store_true", help="skip the 1 MiB-stripe batched leg")
     p.add_argument("--layout", default="256", choices=["odd128", "256"],
                    help="block row stride in HBM: 256-byte multiple (default) or an odd number of 128-byte lines")
+    p.add_argument("--no-row-padding", action="store_true",
+                   help="do not pass FEC_FLAG_ROW_PADDING (rows then end mid-line where sz is not a multiple of 128)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -267,12 +269,15 @@ def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
     return {key: round(v, 1) for key, v in res.items()}
 
 
-def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256"):
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
     to 256 bytes (row_stride), so every block starts 256-byte aligned (the
-    reference's API takes separate buffers per block, which are aligned too)."""
+    reference's API takes separate buffers per block, which are aligned too).
+    row_padding: the calls carry FEC_FLAG_ROW_PADDING, letting the library run
+    each row out to its next 128-byte line inside that padding (whole-line
+    writes; the bytes counted stay k*sz per stripe)."""
     r = m - k
     ld = row_stride(sz, layout)
     gen = torch.Generator(device="cuda").manual_seed(1234 + k)
@@ -285,12 +290,15 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
     rec = torch.empty((ns, nrec, ld), dtype=torch.uint8, device="cuda")
     enc_nums = list(range(k, m))
     code = capi.Code(k, m)
+    fl = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if row_padding else 0)
 
     def enc(sh):
-        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, enc_nums, sz, ns, stream=sh)
+        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, enc_nums, sz, ns, stream=sh,
+                          flags=fl)
 
     def dec(sh):
-        code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, nrec * ld, slots, sz, ns, stream=sh)
+        code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, nrec * ld, slots, sz, ns, stream=sh,
+                          flags=fl)
 
     stream = torch.cuda.current_stream()
     enc(stream.cuda_stream)
@@ -441,7 +449,8 @@ def main():
         ns = s1 - s0
     else:
         ns = nstripes
-    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout)
+    t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout,
+                     row_padding=not args.no_row_padding)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
     value = total_bytes / el / 1e9
@@ -469,7 +478,7 @@ def main():
         "data": "synthetic (torch.randint bytes, resident in HBM)",
         "config": {"workload": "%s: encode (%d->%d blocks) + decode from blocks %s" % (desc, k, r, t["slots"]),
                    "name": args.workload, "k": k, "m": m, "stripe_bytes": stripe, "stripes_per_gpu": ns,
-                   "block_bytes": sz, "block_row_stride": row_stride(sz, args.layout),
+                   "block_bytes": sz, "block_row_stride": row_stride(sz, args.layout), "row_padding": not args.no_row_padding,
                    "parallelism": "stripes sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": round(enc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),

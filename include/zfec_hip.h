@@ -92,6 +92,11 @@ enum {
                                       not only the missing ones: the output is the stripe itself */
 #define FEC_FLAG_HOST_MEMORY 8u    /* every block is host memory (pageable or page-locked): skip the
                                       per-pointer device queries (small calls from Python bytes) */
+#define FEC_FLAG_ROW_PADDING 16u   /* batched calls: every block row may be read (inputs) and written
+                                      (outputs) up to the next multiple of 128 bytes past its end, so
+                                      each row ends on a whole cache line; output bytes past sz are
+                                      then unspecified.  Used only when the block and stripe strides
+                                      leave that much room; otherwise ignored */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);

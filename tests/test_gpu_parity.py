@@ -440,6 +440,47 @@ def test_batch_short_rows_walk(k, m, sz, ns, rows):
     assert rv[:, :, sz:].sum() == 0
 
 
+@pytest.mark.parametrize("k,m,sz,ns,ld,used", [(3, 10, 1366, 300, 1536, True), (3, 10, 1366, 300, 1400, False),
+                                               (2, 6, 5000, 20, 5120, True), (3, 10, 1408, 100, 1536, True),
+                                               (3, 10, 777, 3, 1024, True), (20, 60, 1000, 8, 1024, True)])
+def test_batch_row_padding_flag(k, m, sz, ns, ld, used):
+    """FEC_FLAG_ROW_PADDING: the library may run each row out to its next
+    128-byte line.  Bytes [0, sz) stay bit-exact against the oracle; bytes from
+    the padded end (or from sz when the stride leaves no room and the flag is
+    ignored) to the row stride are guard bytes that must stay zero."""
+    r = m - k
+    pad = -(-sz // 128) * 128 if used else sz
+    rng = np.random.default_rng(sz + ld + ns)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    host = np.zeros((ns, k, ld), dtype=np.uint8)
+    host[:, :, :sz] = data
+    host[:, :, sz:pad] = 0xA5  # input padding the library may read
+    src = torch.from_numpy(host).cuda()
+    dst = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    fl = capi.FEC_FLAG_ASYNC | capi.FEC_FLAG_ROW_PADDING
+    code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns, stream=st,
+                      flags=fl)
+    torch.cuda.synchronize()
+    out = dst.cpu().numpy()
+    assert out[:, :, pad:].sum() == 0
+    for s in range(ns):
+        assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s
+    slots = place(list(range(m - k, m)), k)
+    allb = np.concatenate([data, out[:, :, :sz]], axis=1)
+    recv = np.zeros((ns, k, ld), dtype=np.uint8)
+    recv[:, :, :sz] = allb[:, slots, :]
+    missing = [i for i in range(k) if slots[i] >= k]
+    rec = torch.zeros((ns, len(missing), ld), dtype=torch.uint8, device="cuda")
+    code.decode_batch(torch.from_numpy(recv).cuda().data_ptr(), ld, k * ld, rec.data_ptr(), ld, len(missing) * ld,
+                      slots, sz, ns, stream=st, flags=fl)
+    torch.cuda.synchronize()
+    rv = rec.cpu().numpy()
+    assert (rv[:, :, :sz] == data[:, missing, :]).all()
+    assert rv[:, :, pad:].sum() == 0
+
+
 @pytest.mark.parametrize("k,m,nums", [(3, 10, [7, 1, 9]), (5, 9, [0, 1, 2, 3, 4]), (10, 16, list(range(6, 16)))])
 def test_decode_all_primaries_flag(k, m, nums):
     """FEC_FLAG_ALL_PRIMARIES: the k outputs are the primaries in order, present ones copied."""

@@ -16,12 +16,12 @@ from zfec_amd import capi  # noqa: E402
 # (k, m, block bytes, stripes, row stride)
 SHAPES = [
     (3, 10, 1366, 10 ** 6, 1536),
-    (3, 10, 1366, 10 ** 6, 1408),
-    (3, 10, 1366, 10 ** 6, 1664),
-    (3, 10, 2730, 5 * 10 ** 5, 2816),
-    (3, 10, 2730, 5 * 10 ** 5, 2944),
-    (4, 12, 4096, 3 * 10 ** 5, 4096),
-    (4, 12, 4096, 3 * 10 ** 5, 4224),
+    (3, 10, 1360, 10 ** 6, 1536),
+    (3, 10, 1376, 10 ** 6, 1536),
+    (3, 10, 1408, 10 ** 6, 1536),
+    (3, 10, 1536, 10 ** 6, 1536),
+    (3, 10, 1366, 10 ** 6, 1366),
+    (3, 10, 1408, 10 ** 6, 1408),
 ]
 
 
