@@ -18,8 +18,10 @@ replay measured slower than eager launches).
 
 Multi-GPU (torchrun, one rank per GPU): stripes are independent, so ranks
 never exchange data.  cfg2/cfg3: each rank owns its own stripe (weak
-scaling).  cfg4/cfg5: the fixed batch is split by zfec_amd.shard.shard_range
-(strong scaling).  The only collectives are the timing barrier and the
+scaling); with --slabs the ONE stripe's block byte range is split instead
+(zfec_amd.shard.slab_range, strong scaling: rank r holds columns [c0, c1) of
+every block).  cfg4/cfg5: the fixed batch is split by
+zfec_amd.shard.shard_range (strong scaling).  The only collectives are the timing barrier and the
 max/sum reductions.
 
 Also reported: the dominant kernel's roofline (encode: (k+r)*sz*stripes
@@ -45,7 +47,7 @@ sys.path.insert(0, ROOT)
 
 import zfec_amd  # noqa: E402
 from zfec_amd import capi  # noqa: E402
-from zfec_amd.shard import shard_range  # noqa: E402
+from zfec_amd.shard import shard_range, slab_range  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "encode+decode GB/s (device-resident input) at K/M; % of HBM roofline"
@@ -72,6 +74,9 @@ def parse():
                    help="block row stride in HBM: 256-byte multiple (default) or an odd number of 128-byte lines")
     p.add_argument("--no-row-padding", action="store_true",
                    help="do not pass FEC_FLAG_ROW_PADDING (rows then end mid-line where sz is not a multiple of 128)")
+    p.add_argument("--slabs", action="store_true",
+                   help="cfg2/cfg3 only: split the ONE stripe's block byte range into slabs across the GPUs "
+                        "(zfec_amd.shard.slab_range; strong scaling) instead of one stripe per GPU")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -444,7 +449,14 @@ def main():
     k, m, stripe, nstripes, scaling = WORKLOADS[args.workload]
     r = m - k
     sz = -(-stripe // k)
-    if scaling == "strong":
+    sz_block = sz
+    if args.slabs:
+        if nstripes != 1:
+            raise SystemExit("--slabs applies to the single-stripe workloads (cfg2, cfg3)")
+        # this rank's columns [c0, c1) of every block; held on its GPU as blocks of c1 - c0 bytes
+        c0, c1 = slab_range(sz, world, rank)
+        sz, ns, scaling = c1 - c0, 1, "strong"
+    elif scaling == "strong":
         s0, s1 = shard_range(nstripes, world, rank)
         ns = s1 - s0
     else:
@@ -463,6 +475,8 @@ def main():
             "cfg3": "K=10 M=16, one 256 MiB stripe per GPU",
             "cfg4": "K=20 M=60, 1 GiB = 1024 x 1 MiB stripes split across GPUs",
             "cfg5": "K=3 M=10, 1e6 x 4 KiB objects split across GPUs"}[args.workload]
+    if args.slabs:
+        desc = desc.replace("stripe per GPU", "stripe split into byte-range slabs across GPUs")
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -478,10 +492,13 @@ def main():
         "data": "synthetic (torch.randint bytes, resident in HBM)",
         "config": {"workload": "%s: encode (%d->%d blocks) + decode from blocks %s" % (desc, k, r, t["slots"]),
                    "name": args.workload, "k": k, "m": m, "stripe_bytes": stripe, "stripes_per_gpu": ns,
-                   "block_bytes": sz, "block_row_stride": row_stride(sz, args.layout), "row_padding": not args.no_row_padding,
-                   "parallelism": "stripes sharded across %d GPU(s), no collective" % world},
+                   "block_bytes": sz_block, "slab_bytes_rank0": sz if args.slabs else None,
+                   "block_row_stride": row_stride(sz, args.layout), "row_padding": not args.no_row_padding,
+                   "parallelism": ("block byte range split into %d slabs (%d B on rank 0), one per GPU, no collective"
+                                   % (world, sz) if args.slabs else
+                                   "stripes sharded across %d GPU(s), no collective" % world)},
         "roofline": {"bound": "hbm", "achieved": round(enc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(args.workload),
+                     "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": None if args.slabs else pmc_traffic(args.workload),
                      "kernel": "%s (encode)" % t["kernels"]["encode"], "algorithmic_bytes_per_launch": enc_bytes,
                      "launch_ms": round(t["enc_ms"], 4),
                      "launch_ms_event_pairs": round(t["enc_ms_pairs"], 4),
@@ -495,7 +512,7 @@ def main():
                             "kernel": "%s (decode)" % t["kernels"]["decode"],
                             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4),
                             "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4)},
-        "valu_roofline": valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
+        "valu_roofline": None if args.slabs else valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
         "encode_input_GBps": round(k * sz * ns / (t["enc_ms"] * 1e-3) / 1e9, 1),

@@ -339,6 +339,45 @@ def test_c_abi_device_pointers_misaligned():
         assert int(out[:3].sum()) == 0 and int(out[3 + 7 * sz:].sum()) == 0  # no stray writes
 
 
+@pytest.mark.parametrize("k,m,sz", [(3, 10, 100003), (10, 16, 65539), (20, 60, 4099)])
+def test_slab_split_equals_whole_stripe(k, m, sz):
+    """One stripe split into byte-range slabs (zfec_amd.shard.slab_range, the
+    multi-GPU split of a single huge stripe): each "rank" encodes
+    and decodes its columns with every block pointer advanced to the slab, and
+    the slabs put together equal the whole-stripe result and the oracle."""
+    from zfec_amd.shard import slab_range
+
+    code = capi.Code(k, m)
+    r = m - k
+    rng = np.random.default_rng(k * 1000 + m)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    expect = oracle.encode(k, m, data)
+    src = torch.from_numpy(data).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    secs = list(range(m - k, m))  # the last k blocks
+    for world in (1, 2, 3, 8):
+        par = torch.zeros(r, sz, dtype=torch.uint8, device="cuda")
+        for rank in range(world):
+            c0, c1 = slab_range(sz, world, rank)
+            if c1 > c0:
+                code.encode_ptrs([src[j].data_ptr() + c0 for j in range(k)],
+                                 [par[i].data_ptr() + c0 for i in range(r)], list(range(k, m)), c1 - c0, stream=st)
+        torch.cuda.synchronize()
+        assert (par.cpu().numpy() == expect).all(), world
+        # decode from the last k blocks (secondaries first), slab by slab
+        full = torch.cat([src, par])
+        slots = place(secs, k)
+        missing = [i for i in range(k) if slots[i] != i]
+        rec = torch.zeros(len(missing), sz, dtype=torch.uint8, device="cuda")
+        for rank in range(world):
+            c0, c1 = slab_range(sz, world, rank)
+            if c1 > c0:
+                code.decode_ptrs([full[b].data_ptr() + c0 for b in slots],
+                                 [rec[i].data_ptr() + c0 for i in range(len(missing))], slots, c1 - c0, stream=st)
+        torch.cuda.synchronize()
+        assert torch.equal(rec, src[missing]), world
+
+
 # ---- device-resident tensors through the Python surface -----------------------
 
 def test_torch_tensors_roundtrip():
