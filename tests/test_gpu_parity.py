@@ -441,6 +441,45 @@ def test_batch_encode_decode(k, m, sz, ns):
     assert (rec.cpu().numpy() == data[:, missing, :]).all()
 
 
+@pytest.mark.parametrize("k,m,sz,ns", [(3, 10, 1366, 3000), (10, 16, 333, 50), (20, 60, 77, 40), (1, 3, 5, 7)])
+def test_batch_block_major_layout(k, m, sz, ns):
+    """Block-major batches (block j of every stripe packed back to back: stripe
+    stride == sz, block stride >= ns * sz) run as one long stripe of ns * sz
+    bytes (fec_abi.cpp run_batch): every stripe against the oracle, decode back,
+    and guard bytes between and after the block arrays stay untouched."""
+    code = capi.Code(k, m)
+    r = m - k
+    rng = np.random.default_rng(sz * 7 + ns)
+    data = rng.integers(0, 256, size=(k, ns, sz), dtype=np.uint8)
+    g = 96  # guard bytes after each block array
+    bs = ns * sz + g
+    src = torch.zeros(k * bs, dtype=torch.uint8, device="cuda")
+    for j in range(k):
+        src[j * bs:j * bs + ns * sz] = torch.from_numpy(data[j].reshape(-1)).cuda()
+    dst = torch.full((r * bs,), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(src.data_ptr(), bs, sz, dst.data_ptr(), bs, sz, list(range(k, m)), sz, ns, stream=st)
+    torch.cuda.synchronize()
+    out = dst.cpu().numpy().reshape(r, bs)
+    assert (out[:, ns * sz:] == 0xA5).all(), "write past a block array"
+    par = out[:, :ns * sz].reshape(r, ns, sz)
+    for s in sorted(set([0, ns - 1] + [int(x) for x in rng.integers(0, ns, 5)])):
+        assert (par[:, s] == oracle.encode(k, m, np.ascontiguousarray(data[:, s]))).all(), s
+    # decode every stripe from its last k blocks, same layout
+    slots = place(list(range(m - k, m)), k)
+    allb = np.concatenate([data, par], axis=0)
+    recv = torch.zeros(k * bs, dtype=torch.uint8, device="cuda")
+    for i, b in enumerate(slots):
+        recv[i * bs:i * bs + ns * sz] = torch.from_numpy(np.ascontiguousarray(allb[b]).reshape(-1)).cuda()
+    missing = [i for i in range(k) if slots[i] >= k]
+    rec = torch.full((len(missing) * bs,), 0x5A, dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr(), bs, sz, rec.data_ptr(), bs, sz, slots, sz, ns, stream=st)
+    torch.cuda.synchronize()
+    got = rec.cpu().numpy().reshape(len(missing), bs)
+    assert (got[:, ns * sz:] == 0x5A).all(), "write past a recovered block array"
+    assert (got[:, :ns * sz].reshape(len(missing), ns, sz) == data[missing]).all()
+
+
 @pytest.mark.parametrize("k,m,sz,ns,rows", [(3, 10, 1366, 300, True), (2, 10, 1025, 64, True), (4, 12, 4096, 100, True),
                                             (1, 9, 2049, 80, True), (3, 10, 1024, 100, False), (3, 10, 4097, 70, False),
                                             (3, 10, 1366, 63, False)])

@@ -759,6 +759,14 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     const unsigned k = code->k;
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
     if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    // Block-major batches (stripes packed back to back inside each block array,
+    // both strides == sz) are one stripe of nstripes * sz bytes: output byte x
+    // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so
+    // one long-stream launch replaces the walk over short rows.
+    if (nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
+        sz *= nstripes;
+        nstripes = 1;
+    }
     // FEC_FLAG_ROW_PADDING: run the rows out to a whole 128-byte line where the
     // strides leave room.  A row ending mid-line leaves a partly written line
     // that HBM completes with a read-modify-write: 10^6 K=3/M=10 stripes of
