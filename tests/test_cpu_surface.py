@@ -234,3 +234,20 @@ def test_jit_prepare_concurrent_threads(tmp_path, monkeypatch):
     assert not errors, errors
     assert len(list(tmp_path.glob("zfec_hip_bitslice_k5_r4_*.co"))) == 1
     assert len(list(tmp_path.glob("zfec_hip_bitslice_k6_r5_*.co"))) == 1
+
+
+def test_tensor_batch_api_preconditions():
+    """The batched tensor entry points reject host tensors and wrong shapes
+    before any GPU work (no GPU needed)."""
+    import torch
+    import zfec_amd
+
+    enc = zfec_amd.Encoder(3, 10)
+    with pytest.raises(zfec_amd.Error):
+        enc.encode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8))  # host tensor
+    with pytest.raises(zfec_amd.Error):
+        enc.encode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8), [1])  # primary requested
+    with pytest.raises(zfec_amd.Error):
+        zfec_amd.Decoder(3, 10).decode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8), [1, 0, 5])
+    with pytest.raises(TypeError):
+        zfec_amd.Decoder(3, 10).decode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8), 5)

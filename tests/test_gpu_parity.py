@@ -688,3 +688,42 @@ def test_reference_binding_dropin(golden):
         nums = c["decode_nums"][0]
         dec = ref_api.Decoder(k, m).decode([allb[n].tobytes() for n in nums], nums)
         assert b"".join(bytes(x) for x in dec) == inp.tobytes()
+
+
+@pytest.mark.parametrize("k,m,sz,ns,block_major", [(3, 10, 1366, 500, False), (3, 10, 1366, 500, True),
+                                                   (10, 16, 4000, 9, True), (20, 60, 777, 6, False)])
+def test_tensor_batch_api(k, m, sz, ns, block_major):
+    """zfec_amd.Encoder.encode_batch / Decoder.decode_batch on [nstripes, k, sz]
+    device tensors (object-major, or a transposed block-major array): parity
+    against the oracle for sampled stripes, decode back from the last k blocks."""
+    rng = np.random.default_rng(ns * 31 + sz)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    t = torch.from_numpy(data).cuda()
+    if block_major:
+        t = t.transpose(0, 1).contiguous().transpose(0, 1)  # storage [k][ns][sz]
+    enc = zfec_amd.Encoder(k, m)
+    par = enc.encode_batch(t)
+    assert par.shape == (ns, m - k, sz) and (par.stride(0) < par.stride(1)) == block_major
+    torch.cuda.synchronize()
+    p = par.cpu().numpy()
+    for s in sorted(set([0, ns - 1] + [int(x) for x in rng.integers(0, ns, 4)])):
+        assert (p[s] == oracle.encode(k, m, data[s])).all(), s
+    sub = enc.encode_batch(t, [m - 1, k])
+    assert torch.equal(sub[:, 0], par[:, m - 1 - k]) and torch.equal(sub[:, 1], par[:, 0])
+    slots = place(list(range(m - k, m)), k)
+    allb = torch.cat([t, par], dim=1)
+    recv = allb[:, slots, :]
+    if block_major:
+        recv = recv.transpose(0, 1).contiguous().transpose(0, 1)
+    else:
+        recv = recv.contiguous()
+    rec = zfec_amd.Decoder(k, m).decode_batch(recv, slots)
+    torch.cuda.synchronize()
+    missing = [i for i in range(k) if slots[i] >= k]
+    assert (rec.cpu().numpy() == data[:, missing, :]).all()
+    with pytest.raises(zfec_amd.Error):
+        enc.encode_batch(t, [0])  # primaries are not produced by the batch call
+    if k > 1 and m - k >= 2:
+        bad = [1, 0] + list(range(k, k + k - 2)) if k > 2 else [1, 0]
+        with pytest.raises(zfec_amd.Error):
+            zfec_amd.Decoder(k, m).decode_batch(recv, bad)  # primary off its slot

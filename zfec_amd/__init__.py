@@ -66,6 +66,42 @@ def _device_blocks(blocks, k):
     return bl, sz, dev
 
 
+def _batch_view(blocks, nblocks, what):
+    """Check a [nstripes, nblocks, sz] uint8 device tensor for the batched entry
+    points; any strides with unit stride along sz, so a transposed block-major
+    [nblocks, nstripes, sz] array passes as is (fec_encode_batch runs it as one
+    long stripe).  Returns (nstripes, sz, block stride, stripe stride)."""
+    import torch
+
+    if not _is_device_tensor(blocks) or blocks.dtype != torch.uint8 or blocks.dim() != 3:
+        raise Error("Precondition violation: %s is required to be a uint8 device tensor [nstripes, %d, sz]"
+                    % (what, nblocks))
+    ns, nb, sz = blocks.shape
+    if nb != nblocks:
+        raise Error("Precondition violation: %s is required to hold %d blocks per stripe, not %d" % (what, nblocks, nb))
+    if sz > 1 and blocks.stride(2) != 1:
+        raise Error("Precondition violation: %s blocks are required to be contiguous along sz" % what)
+    return ns, sz, blocks.stride(1), blocks.stride(0)
+
+
+def _batch_out(like_block_major, ns, nb, sz, device):
+    """Output tensor [ns, nb, sz]: block-major storage when the input was."""
+    import torch
+
+    if like_block_major:
+        return torch.empty((nb, ns, sz), dtype=torch.uint8, device=device).transpose(0, 1)
+    return torch.empty((ns, nb, sz), dtype=torch.uint8, device=device)
+
+
+def _capi_code(coder):
+    code = getattr(coder, "_batch_code", None)
+    if code is None:
+        from . import capi
+
+        code = coder._batch_code = capi.Code(coder.k, coder.m)
+    return code
+
+
 class Encoder(_fec.Encoder):
     """Encoder(k, m) -- see zfec/_fecmodule.c:40-44."""
 
@@ -77,6 +113,31 @@ class Encoder(_fec.Encoder):
         if first is None or not _is_device_tensor(first):
             return _fec.Encoder.encode(self, inblocks, desired_blocks_nums)
         return self._encode_device(list(inblocks), desired_blocks_nums)
+
+    def encode_batch(self, blocks, desired_blocks_nums=None):
+        """Encode many independent stripes in one launch (fec_encode_batch).
+
+        blocks: uint8 device tensor [nstripes, k, sz] (any strides with unit
+        stride along sz; a transposed block-major [k, nstripes, sz] array is the
+        fastest layout).  desired_blocks_nums: secondary block numbers in
+        [k, m-1] (default k..m-1).  Returns a new [nstripes, len(desired), sz]
+        tensor, block-major when the input was; work is enqueued on the current
+        stream.  A batched counterpart of encode() for many small objects
+        (SURVEY.md §8f row 2); no reference equivalent."""
+        from . import capi
+
+        k, m = self.k, self.m
+        nums = list(range(k, m)) if desired_blocks_nums is None else list(desired_blocks_nums)
+        for x in nums:
+            if not isinstance(x, int) or x < k or x >= m:
+                raise Error("Precondition violation: encode_batch desired block nums are required to be secondary "
+                            "block nums in [k, m-1] = [%d, %d], but one was %r" % (k, m - 1, x))
+        ns, sz, sbs, sss = _batch_view(blocks, k, "blocks")
+        out = _batch_out(sss < sbs, ns, len(nums), sz, blocks.device)
+        if nums and ns and sz:
+            _capi_code(self).encode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1), out.stride(0),
+                                          nums, sz, ns, stream=_stream_handle(blocks.device), flags=capi.FEC_FLAG_ASYNC)
+        return out
 
     def _encode_device(self, inblocks, desired):
         import torch
@@ -119,6 +180,38 @@ class Decoder(_fec.Decoder):
         if first is None or not _is_device_tensor(first):
             return _fec.Decoder.decode(self, blocks, blocknums)
         return self._decode_device(list(blocks), blocknums)
+
+    def decode_batch(self, blocks, blocknums):
+        """Decode many independent stripes that all received the same block
+        numbers, in one launch (fec_decode_batch).
+
+        blocks: uint8 device tensor [nstripes, k, sz] (strides as in
+        Encoder.encode_batch), slot j of every stripe holding block blocknums[j];
+        a primary block must sit at its own slot (primary i at slot i, as
+        fec_decode requires, zfec/fec.c:549).  Returns a new [nstripes, r, sz]
+        tensor of the r missing primaries in ascending order."""
+        from . import capi
+
+        k, m = self.k, self.m
+        try:
+            nums = list(blocknums)
+        except TypeError:
+            raise TypeError("Second argument was not a sequence.")
+        if len(nums) != k or len(set(nums)) != k:
+            raise Error("Precondition violation: blocknums is required to hold k = %d distinct block nums" % k)
+        for i, x in enumerate(nums):
+            if not isinstance(x, int) or x < 0 or x >= m:
+                raise Error("Precondition violation: block nums are required to be in [0, m-1] = [0, %d], but one "
+                            "was %r" % (m - 1, x))
+            if x < k and x != i:
+                raise Error("Precondition violation: decode_batch requires primary block %d at slot %d" % (x, x))
+        ns, sz, sbs, sss = _batch_view(blocks, k, "blocks")
+        r = sum(1 for x in nums if x >= k)
+        out = _batch_out(sss < sbs, ns, r, sz, blocks.device)
+        if r and ns and sz:
+            _capi_code(self).decode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1), out.stride(0),
+                                          nums, sz, ns, stream=_stream_handle(blocks.device), flags=capi.FEC_FLAG_ASYNC)
+        return out
 
     def _decode_device(self, blocks, blocknums):
         import torch
