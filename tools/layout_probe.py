@@ -11,7 +11,10 @@ encode + last-k decode step as bench.py:
 GB/s = 2 * k * sz * stripes / (step time), events around `steps` steps after
 warmup.  Both layouts are checked against each other (decode(encode(x)) == x).
 
-usage: python tools/layout_probe.py [--stripes 1000000] [--steps 20] [--rounds 3]
+--shape cfg4 runs the same comparison for 1024 K=20/M=60 stripes of 1 MiB
+(sz = 52,429; bench rows of 52,480 bytes).
+
+usage: python tools/layout_probe.py [--shape cfg5|cfg4] [--stripes N] [--steps 20] [--rounds 3]
 """
 import argparse
 import json
@@ -50,14 +53,16 @@ def timed(step, steps, warmup):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--stripes", type=int, default=1000000)
+    p.add_argument("--shape", default="cfg5", choices=["cfg5", "cfg4"])
+    p.add_argument("--stripes", type=int, default=0)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rounds", type=int, default=3)
     a = p.parse_args()
-    k, m, ns = 3, 10, a.stripes
+    k, m, stripe, ns = {"cfg5": (3, 10, 4096, 1000000), "cfg4": (20, 60, 1 << 20, 1024)}[a.shape]
+    ns = a.stripes or ns
     r = m - k
-    sz = -(-4096 // k)
+    sz = -(-stripe // k)
     code = capi.Code(k, m)
     slots = place(list(range(m - k, m)), k)
     missing = [i for i in range(k) if slots[i] >= k]
@@ -66,7 +71,7 @@ def main():
     fl = capi.FEC_FLAG_ASYNC
 
     # object-major, as bench.py
-    ld = 1536
+    ld = -(-sz // 256) * 256  # bench.py row_stride
     o_data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen)
     o_par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
     o_recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
@@ -107,6 +112,17 @@ def main():
     assert torch.equal(b_rec, b_data[missing]), "block-major decode(encode(x)) != x"
     assert torch.equal(o_rec[:, :, :sz], o_data[:, missing, :sz]), "object-major decode(encode(x)) != x"
 
+    # wide codes: the second large launch of a matrix queues its bit-sliced
+    # kernel's compile (as in bench.py); wait for it, then check again
+    o_step()
+    b_step()
+    capi.jit_wait()
+    b_par.zero_()
+    o_step()
+    b_step()
+    torch.cuda.synchronize()
+    assert torch.equal(b_par, o_par[:, :, :sz].permute(1, 0, 2)), "layouts disagree on parity (JIT kernels)"
+    assert torch.equal(b_rec, b_data[missing]), "block-major decode(encode(x)) != x (JIT kernels)"
     res = {"object_major_ms": [], "block_major_ms": []}
     for _ in range(a.rounds):
         res["object_major_ms"].append(round(timed(o_step, a.steps, a.warmup), 4))
@@ -122,7 +138,7 @@ def main():
     for key in ("object_major", "block_major"):
         ms = sorted(res[key + "_ms"])[len(res[key + "_ms"]) // 2]
         res[key + "_GBps"] = round(byts / (ms * 1e-3) / 1e9, 1)
-    res.update({"stripes": ns, "sz": sz, "encode_kernel_object_major": ko, "encode_kernel_block_major": kb})
+    res.update({"collapse": os.environ.get("ZFEC_HIP_BATCH_COLLAPSE", "1"), "shape": a.shape, "k": k, "m": m, "stripes": ns, "sz": sz, "encode_kernel_object_major": ko, "encode_kernel_block_major": kb})
     print(json.dumps(res))
 
 

@@ -763,7 +763,12 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     // both strides == sz) are one stripe of nstripes * sz bytes: output byte x
     // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so
     // one long-stream launch replaces the walk over short rows.
-    if (nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
+    // (ZFEC_HIP_BATCH_COLLAPSE=0 turns this off, for A/B runs.)
+    static const bool collapse = [] {
+        const char* v = getenv("ZFEC_HIP_BATCH_COLLAPSE");
+        return !(v && v[0] == '0');
+    }();
+    if (collapse && nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
         sz *= nstripes;
         nstripes = 1;
     }
