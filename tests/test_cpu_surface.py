@@ -251,3 +251,60 @@ def test_tensor_batch_api_preconditions():
         zfec_amd.Decoder(3, 10).decode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8), [1, 0, 5])
     with pytest.raises(TypeError):
         zfec_amd.Decoder(3, 10).decode_batch(torch.zeros((4, 3, 16), dtype=torch.uint8), 5)
+
+
+@pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")
+def test_batch_library_errors_are_zfec_errors():
+    """Library failures inside the batched tensor entry points (here: no GPU)
+    surface as zfec_amd.Error, not as the ctypes layer's FecError."""
+    enc = zfec_amd.Encoder(3, 10)
+    with pytest.raises(zfec_amd.Error, match="no GPU"):
+        with zfec_amd._as_error():
+            zfec_amd._capi_code(enc).encode_batch(0x1000, 16, 48, 0x2000, 16, 112, list(range(3, 10)), 16, 4)
+    with pytest.raises(zfec_amd.Error, match="no GPU"):
+        with zfec_amd._as_error():
+            zfec_amd._capi_code(zfec_amd.Decoder(3, 10)).decode_batch(0x1000, 16, 48, 0x2000, 16, 48, [3, 4, 5],
+                                                                     16, 4)
+
+
+_DROPIN_CHILD = r"""
+import glob, importlib.util, sys
+spec = importlib.util.spec_from_file_location("zfec_dropin._fec", sys.argv[1])
+mod = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(mod)
+for _ in range(2):
+    out = mod.Encoder(3, 10).encode([b"abc", b"def", b"ghi"])
+    assert len(out) == 10
+    dec = mod.Decoder(3, 10).decode([b"abc", b"def", b"ghi"], [3, 4, 5])
+print("returned")
+"""
+
+
+@pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")
+@pytest.mark.parametrize("quiet", [False, True])
+def test_void_entry_points_report_failures(quiet):
+    """fec_encode / fec_decode return void (zfec/fec.h:49,57) and the
+    reference's own binding never asks for a status: with no GPU, the
+    reference's unmodified _fecmodule.c linked to libzfec_hip.so must see a
+    diagnostic on stderr, once per entry point (ZFEC_HIP_QUIET=1 silences it)."""
+    import glob
+    import sys
+
+    paths = glob.glob(os.path.join(ROOT, "oracle", "_ref", "dropin", "_fec*.so"))
+    if not paths:
+        pytest.skip("oracle/_ref/dropin not built (needs /root/reference at build time)")
+    env = dict(os.environ)
+    env.pop("ZFEC_HIP_QUIET", None)
+    if quiet:
+        env["ZFEC_HIP_QUIET"] = "1"
+    res = subprocess.run([sys.executable, "-c", _DROPIN_CHILD, paths[0]], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert "returned" in res.stdout
+    enc = [ln for ln in res.stderr.splitlines() if "zfec_hip: fec_encode failed" in ln]
+    dec = [ln for ln in res.stderr.splitlines() if "zfec_hip: fec_decode failed" in ln]
+    if quiet:
+        assert not enc and not dec, res.stderr
+    else:
+        assert len(enc) == 1 and len(dec) == 1, res.stderr
+        assert "status 2" in enc[0] and "no GPU" in enc[0]

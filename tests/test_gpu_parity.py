@@ -480,6 +480,75 @@ def test_batch_block_major_layout(k, m, sz, ns):
     assert (got[:, :ns * sz].reshape(len(missing), ns, sz) == data[missing]).all()
 
 
+_LAYOUTS = {
+    # block-major, the input block arrays overlapping (block stride < ns * sz):
+    # the collapse runs them as one long stripe per block
+    "block_major_aliased_inputs": dict(k=3, m=10, sz=1366, ns=3000, in_bs=1366 * 1500 + 5, in_ss=1366,
+                                       out_bs=1366 * 3000 + 64, out_ss=1366, seed=11, guard=96),
+    # block-major with FEC_FLAG_ROW_PADDING: the collapsed row must not run past
+    # the grant of the last stripe (the flag's per-row room is absent here)
+    "block_major_row_padding": dict(k=3, m=10, sz=1366, ns=3000, in_bs=1366 * 3000, in_ss=1366,
+                                    out_bs=1366 * 3000, out_ss=1366, seed=12, guard=128, flags=16),
+    # one long stripe and many object-major stripes, cut into many launches
+    # when the per-launch unit limit is lowered
+    "one_stripe": dict(k=10, m=16, sz=3 * 1024 * 1024 + 77, ns=1, in_bs=3 * 1024 * 1024 + 128, in_ss=0,
+                       out_bs=3 * 1024 * 1024 + 128, out_ss=0, seed=13, guard=96),
+    "object_major": dict(k=4, m=9, sz=5000, ns=700, in_bs=5000, in_ss=4 * 5000, out_bs=5000, out_ss=5 * 5000,
+                         seed=14, guard=96),
+}
+
+
+def _run_child(spec, env_extra, tmp_path, tag):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / ("%s.npy" % tag)
+    env = dict(os.environ)
+    env.update(env_extra)
+    res = subprocess.run([sys.executable, os.path.join(root, "tests", "gpu_batch_child.py"), json.dumps(spec),
+                          str(out)], env=env, capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stderr[-2000:]
+    return np.load(out), res.stdout.strip()
+
+
+@pytest.mark.parametrize("layout", sorted(_LAYOUTS))
+def test_batch_layout_env_variants(layout, tmp_path):
+    """The same fec_encode_batch run three ways, each in its own process since
+    the knobs are read once: as shipped, with the block-major collapse off
+    (ZFEC_HIP_BATCH_COLLAPSE=0), and with at most 1024 units per launch
+    (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte ranges, batches
+    into stripe groups).  All three outputs, guard bytes included, must be
+    identical, and sampled stripes must equal the oracle's parity."""
+    import importlib.util
+    import os
+
+    spec = _LAYOUTS[layout]
+    base, kern = _run_child(spec, {}, tmp_path, "base")
+    nocol, _ = _run_child(spec, {"ZFEC_HIP_BATCH_COLLAPSE": "0"}, tmp_path, "nocollapse")
+    split, _ = _run_child(spec, {"ZFEC_HIP_LAUNCH_UNITS": "1024"}, tmp_path, "split")
+    assert np.array_equal(base, nocol), "collapse changed the output"
+    assert np.array_equal(base, split), "launch splitting changed the output"
+    child = importlib.util.spec_from_file_location(
+        "gpu_batch_child", os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpu_batch_child.py"))
+    mod = importlib.util.module_from_spec(child)
+    child.loader.exec_module(mod)
+    src = mod.src_bytes(spec)
+    k, m, sz, ns = spec["k"], spec["m"], spec["sz"], spec["ns"]
+    r = m - k
+    end = (ns - 1) * spec["out_ss"] + (r - 1) * spec["out_bs"] + sz
+    assert (base[end:] == 0xA5).all(), "write past the last output row"
+    rng = np.random.default_rng(spec["seed"])
+    for s in sorted(set([0, ns - 1] + [int(x) for x in rng.integers(0, ns, 6)])):
+        ins = np.stack([src[s * spec["in_ss"] + j * spec["in_bs"]:][:sz] for j in range(k)])
+        want = oracle.encode(k, m, ins)
+        for i in range(r):
+            o = s * spec["out_ss"] + i * spec["out_bs"]
+            assert (base[o:o + sz] == want[i]).all(), (s, i, kern)
+
+
 @pytest.mark.parametrize("k,m,sz,ns,rows", [(3, 10, 1366, 300, True), (2, 10, 1025, 64, True), (4, 12, 4096, 100, True),
                                             (1, 9, 2049, 80, True), (3, 10, 1024, 100, False), (3, 10, 4097, 70, False),
                                             (3, 10, 1366, 63, False)])
@@ -596,12 +665,46 @@ def test_config2_64mib_vs_oracle():
     assert (torch.stack(dec).cpu().numpy() == data).all()
 
 
-def _batched_full_size(k, m, S, ns, seed, sample):
+class _kernels(object):
+    """Which kernel family serves a full-size launch: "jit" = the run-time
+    specialised bit-sliced kernel of the launch's matrix (compiled up front with
+    fec_jit_prepare_*, as bench.py times it), "table" = the JIT off (the kernels
+    a launch falls back on).  check(what) asserts the last launch's kernel."""
+
+    PREFIX = {"jit": "zfec_hip_bitslice", "table": "matapply_"}
+
+    def __init__(self, kind):
+        self.kind = kind
+
+    def __enter__(self):
+        self.prev = capi.jit_mode(capi.JIT_AUTO if self.kind == "jit" else capi.JIT_OFF)
+        return self
+
+    def __exit__(self, *exc):
+        capi.jit_mode(self.prev)
+        return False
+
+    def prepare(self, code, enc_nums=None, dec_slots=None):
+        if self.kind == "jit":
+            if enc_nums is not None:
+                code.jit_prepare_encode(enc_nums)
+            if dec_slots is not None:
+                code.jit_prepare_decode(dec_slots)
+
+    def check(self, what):
+        torch.cuda.synchronize()
+        name = capi.last_kernel_name()
+        assert name.startswith(self.PREFIX[self.kind]), (what, self.kind, name)
+        return name
+
+
+def _batched_full_size(k, m, S, ns, seed, sample, kernels=None):
     """BASELINE batched configs at full size: one encode launch over all
     stripes ([stripe][block][row] rows 256-byte aligned, as bench.py lays them
     out), a decode from the last k blocks; the decode must return every
-    stripe (device-side equality), and sampled stripes' parity must equal
-    the oracle's."""
+    stripe (device-side equality), and sampled stripes' parity and recovered
+    blocks must equal the oracle's.  With `kernels`, the kernel family of both
+    launches is fixed and asserted."""
     r = m - k
     sz = -(-S // k)
     ld = -(-sz // 256) * 256
@@ -609,15 +712,21 @@ def _batched_full_size(k, m, S, ns, seed, sample):
     data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=g)
     par = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
     code = capi.Code(k, m)
+    slots = place(list(range(m - k, m)), k)
+    if kernels:
+        kernels.prepare(code, list(range(k, m)), slots)
     st = torch.cuda.current_stream().cuda_stream
     code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns, stream=st)
-    slots = place(list(range(m - k, m)), k)
+    if kernels:
+        kernels.check("encode")
     recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
     for i, s in enumerate(slots):
         recv[:, i].copy_(data[:, s] if s < k else par[:, s - k])
     missing = [i for i in range(k) if slots[i] >= k]
     rec = torch.zeros((ns, len(missing), ld), dtype=torch.uint8, device="cuda")
     code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, len(missing) * ld, slots, sz, ns, stream=st)
+    if kernels:
+        kernels.check("decode")
     torch.cuda.synchronize()
     assert bool(torch.equal(rec[:, :, :sz], data[:, missing, :sz]))
     assert int(par[:, :, sz:].count_nonzero()) == 0  # nothing written past the block ends
@@ -625,11 +734,17 @@ def _batched_full_size(k, m, S, ns, seed, sample):
     for s in sorted(set(int(x) for x in rng.integers(0, ns, size=sample))) + [0, ns - 1]:
         got = par[s, :, :sz].cpu().numpy()
         assert (got == oracle.encode(k, m, data[s, :, :sz].cpu().numpy())).all(), s
+        rv = rec[s, :, :sz].cpu().numpy()
+        assert (rv == oracle.decode(k, m, recv[s, :, :sz].cpu().numpy(), slots)).all(), s
 
 
-def test_config4_1024_stripes_of_1mib():
-    """cfg4: K=20/M=60, 1024 x 1 MiB stripes in one launch."""
-    _batched_full_size(20, 60, 1 << 20, 1024, 4, sample=6)
+@pytest.mark.parametrize("kind", ["jit", "table"])
+def test_config4_1024_stripes_of_1mib(kind):
+    """cfg4: K=20/M=60, 1024 x 1 MiB stripes in one launch, on the kernel
+    bench.py times (the bit-sliced kernel of the matrix) and on the table
+    kernel."""
+    with _kernels(kind) as kn:
+        _batched_full_size(20, 60, 1 << 20, 1024, 4, sample=6, kernels=kn)
 
 
 def test_config5_1e6_objects_of_4kib():
@@ -637,22 +752,36 @@ def test_config5_1e6_objects_of_4kib():
     _batched_full_size(3, 10, 4096, 10 ** 6, 5, sample=200)
 
 
-def test_config3_256mib_roundtrip():
+@pytest.mark.parametrize("kind", ["jit", "table"])
+def test_config3_256mib_roundtrip(kind):
     """K=10/M=16, 256 MiB: encode, drop primaries 0-5, decode; compare by
-    equality on the device (size-independent property) and spot-check parity
-    rows against the oracle on a slice (column independence)."""
+    equality on the device (size-independent property) and check parity rows
+    and recovered blocks against the oracle on slices at the start, middle and
+    end (column independence), on the kernel bench.py times and on the table
+    kernel."""
     k, m, S = 10, 16, 256 << 20
     sz = -(-S // k)
     g = torch.Generator(device="cuda").manual_seed(3)
     data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda", generator=g)
     ins = [data[i] for i in range(k)]
-    out = zfec_amd.Encoder(k, m).encode(ins)
     nums = list(range(10, 16)) + [6, 7, 8, 9]
-    dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+    slots = place(nums, k)
+    with _kernels(kind) as kn:
+        kn.prepare(capi.Code(k, m), list(range(k, m)), slots)
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        kn.check("encode")
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        kn.check("decode")
     assert bool(torch.equal(torch.stack(dec), data))
-    lo, hi = sz // 2, sz // 2 + 100000
-    par = torch.stack(out[k:])[:, lo:hi].cpu().numpy()
-    assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all()
+    allb = torch.stack(out)
+    for lo in (0, sz // 2, sz - 100000):
+        hi = lo + 100000
+        par = allb[k:, lo:hi].cpu().numpy()
+        assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all(), lo
+        missing = [i for i in range(k) if slots[i] >= k]
+        got = torch.stack(dec)[missing, lo:hi].cpu().numpy()
+        recv = allb[slots, lo:hi].cpu().numpy()
+        assert (got == oracle.decode(k, m, recv, slots)).all(), lo
 
 
 # ---- the reference's own binding on top of the engine ---------------------------

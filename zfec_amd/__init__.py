@@ -93,12 +93,29 @@ def _batch_out(like_block_major, ns, nb, sz, device):
     return torch.empty((ns, nb, sz), dtype=torch.uint8, device=device)
 
 
+class _as_error(object):
+    """Library failures of the batched entry points (capi.FecError: no GPU,
+    cross-device tensors, ...) surface as zfec_amd.Error like every other
+    failure of this API."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        from . import capi
+
+        if et is not None and issubclass(et, capi.FecError):
+            raise Error(str(ev)) from ev
+        return False
+
+
 def _capi_code(coder):
     code = getattr(coder, "_batch_code", None)
     if code is None:
         from . import capi
 
-        code = coder._batch_code = capi.Code(coder.k, coder.m)
+        with _as_error():
+            code = coder._batch_code = capi.Code(coder.k, coder.m)
     return code
 
 
@@ -135,8 +152,10 @@ class Encoder(_fec.Encoder):
         ns, sz, sbs, sss = _batch_view(blocks, k, "blocks")
         out = _batch_out(sss < sbs, ns, len(nums), sz, blocks.device)
         if nums and ns and sz:
-            _capi_code(self).encode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1), out.stride(0),
-                                          nums, sz, ns, stream=_stream_handle(blocks.device), flags=capi.FEC_FLAG_ASYNC)
+            with _as_error():
+                _capi_code(self).encode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1),
+                                              out.stride(0), nums, sz, ns, stream=_stream_handle(blocks.device),
+                                              flags=capi.FEC_FLAG_ASYNC)
         return out
 
     def _encode_device(self, inblocks, desired):
@@ -209,8 +228,10 @@ class Decoder(_fec.Decoder):
         r = sum(1 for x in nums if x >= k)
         out = _batch_out(sss < sbs, ns, r, sz, blocks.device)
         if r and ns and sz:
-            _capi_code(self).decode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1), out.stride(0),
-                                          nums, sz, ns, stream=_stream_handle(blocks.device), flags=capi.FEC_FLAG_ASYNC)
+            with _as_error():
+                _capi_code(self).decode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1),
+                                              out.stride(0), nums, sz, ns, stream=_stream_handle(blocks.device),
+                                              flags=capi.FEC_FLAG_ASYNC)
         return out
 
     def _decode_device(self, blocks, blocknums):

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -203,20 +204,56 @@ struct DeviceGuard {
 };
 
 // ---- the engine: apply an r x k matrix to k blocks -----------------------------
-//
+
+constexpr size_t align_up_4k(size_t x) { return (x + 4095) / 4096 * 4096; }
+
 // in[j] / out[i] are device pointers (block bases of stripe 0); stripes are
 // in_sstride / out_sstride apart.  Splits into launches that respect the
 // kernel's limits: <= kMaxIn inputs (later input groups XOR-accumulate),
-// <= kMaxOut outputs and <= kMaxCoef coefficients per launch, and < 2^32
-// 16-byte units per launch.
+// <= kMaxOut outputs and <= kMaxCoef coefficients per launch, and at most
+// launch_units() kMinChunk-byte units per launch.  Blocks longer than that
+// are cut into byte ranges of their own launches: output byte x depends only
+// on byte x of the inputs (zfec/fec.c:494-503, :547-556).
+size_t launch_units() {
+    // ZFEC_HIP_LAUNCH_UNITS lowers the limit so tests reach the split paths
+    // with small buffers; the kernels' own bound is < 2^32 units per launch.
+    static const size_t units = [] {
+        const char* v = getenv("ZFEC_HIP_LAUNCH_UNITS");
+        const unsigned long long u = v && *v ? strtoull(v, nullptr, 10) : 0;
+        return u >= 1024 && u < (1ull << 31) ? static_cast<size_t>(u) : size_t(1) << 31;
+    }();
+    return units;
+}
+
+int apply_matrix_range(const uint8_t* coef, unsigned k, unsigned r, const uint8_t* const* in, uint8_t* const* out,
+                       size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride, hipStream_t stream);
+
 int apply_matrix(const uint8_t* coef /* r x k */, unsigned k, unsigned r, const uint8_t* const* in,
                  uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
                  hipStream_t stream) {
     if (r == 0 || sz == 0 || nstripes == 0) return FEC_OK;
     const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
-    const size_t max_units = size_t(1) << 31;
-    const size_t stripes_per_launch = std::max<size_t>(1, max_units / cps);
-    if (cps > max_units) return set_status(FEC_EINVAL, "block size %zu too large for one launch", sz);
+    const size_t max_units = launch_units();
+    if (cps <= max_units) return apply_matrix_range(coef, k, r, in, out, sz, nstripes, in_sstride, out_sstride, stream);
+    // near-equal byte ranges on 4 KiB boundaries, each within the unit limit
+    const size_t pieces = (cps + max_units - 1) / max_units;
+    const size_t piece = align_up_4k((sz + pieces - 1) / pieces);
+    std::vector<const uint8_t*> pin(k);
+    std::vector<uint8_t*> pout(r);
+    for (size_t b0 = 0; b0 < sz; b0 += piece) {
+        const size_t len = std::min(piece, sz - b0);
+        for (unsigned j = 0; j < k; ++j) pin[j] = in[j] + b0;
+        for (unsigned i = 0; i < r; ++i) pout[i] = out[i] + b0;
+        if (apply_matrix_range(coef, k, r, pin.data(), pout.data(), len, nstripes, in_sstride, out_sstride, stream))
+            return t_status;
+    }
+    return FEC_OK;
+}
+
+int apply_matrix_range(const uint8_t* coef, unsigned k, unsigned r, const uint8_t* const* in, uint8_t* const* out,
+                       size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride, hipStream_t stream) {
+    const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
+    const size_t stripes_per_launch = std::max<size_t>(1, launch_units() / cps);
     for (unsigned j0 = 0; j0 < k; j0 += kMaxIn) {
         const unsigned kg = std::min<unsigned>(kMaxIn, k - j0);
         const unsigned rmax = std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
@@ -629,9 +666,32 @@ FEC_API int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fe
     return run_single(rows.data(), code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
 }
 
+namespace {
+// fec.h's fec_encode / fec_decode return void and their callers (the
+// reference's _fecmodule.c, the Haskell binding) never ask for a status, so a
+// failure there would hand back unwritten output buffers in silence.  The
+// first failure of each entry point is reported on stderr (once per process;
+// ZFEC_HIP_QUIET=1 silences it); fec_last_status() still holds every one.
+void report_void_failure(const char* fn, int st) {
+    static std::atomic<int> reported[2] = {{0}, {0}};
+    static const bool quiet = [] {
+        const char* v = getenv("ZFEC_HIP_QUIET");
+        return v && v[0] == '1';
+    }();
+    std::atomic<int>& once = reported[fn[4] == 'd' ? 1 : 0];
+    if (quiet || once.exchange(1) != 0) return;
+    fprintf(stderr,
+            "zfec_hip: %s failed (status %d: %s); its output blocks are not valid.  Further failures of %s are "
+            "not reported here; fec_last_status() / fec_last_error_message() give each call's status.\n",
+            fn, st, t_msg, fn);
+    fflush(stderr);
+}
+}  // namespace
+
 FEC_API void fec_encode(const fec_t* code, const gf* const* src, gf* const* fecs, const unsigned* block_nums,
                         size_t num_block_nums, size_t sz) {
-    (void)fec_encode_ex(code, src, fecs, block_nums, num_block_nums, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
+    const int st = fec_encode_ex(code, src, fecs, block_nums, num_block_nums, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
+    if (st != FEC_OK) report_void_failure("fec_encode", st);
 }
 
 FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
@@ -647,7 +707,8 @@ FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const*
 
 FEC_API void fec_decode(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
                         size_t sz) {
-    (void)fec_decode_ex(code, inpkts, outpkts, index, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
+    const int st = fec_decode_ex(code, inpkts, outpkts, index, sz, nullptr, FEC_FLAG_LIBRARY_STREAM);
+    if (st != FEC_OK) report_void_failure("fec_decode", st);
 }
 
 FEC_API void build_decode_matrix_into_space(const fec_t* code, const unsigned* index, const unsigned k, gf* matrix) {
@@ -768,20 +829,27 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
         const char* v = getenv("ZFEC_HIP_BATCH_COLLAPSE");
         return !(v && v[0] == '0');
     }();
-    if (collapse && nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
-        sz *= nstripes;
-        nstripes = 1;
-    }
     // FEC_FLAG_ROW_PADDING: run the rows out to a whole 128-byte line where the
     // strides leave room.  A row ending mid-line leaves a partly written line
     // that HBM completes with a read-modify-write: 10^6 K=3/M=10 stripes of
     // 1366-byte blocks in 1536-byte rows encode in 2.91 ms, of 1408-byte blocks
     // in 2.55 ms (tools/grid_probe.py, profiles/r01_grid_probe_sz.log).
+    // `grant`: bytes past a row's start the flag lets us touch (per row).
+    size_t grant = sz;
     if (flags & FEC_FLAG_ROW_PADDING) {
         const size_t padded = (sz + 127) / 128 * 128;
         const bool room = sbs >= padded && dbs >= padded && (nstripes == 1 || (sss >= (k - 1) * sbs + padded &&
                                                                                 dss >= (r - 1) * dbs + padded));
-        if (room) sz = padded;
+        if (room) grant = padded;
+    }
+    if (collapse && nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
+        // the collapsed row may run out to its own next line only inside the
+        // last stripe's grant: (nstripes - 1) * sz + grant
+        const size_t len = sz * nstripes, padded = (len + 127) / 128 * 128;
+        sz = padded <= len - sz + grant ? padded : len;
+        nstripes = 1;
+    } else {
+        sz = grant;
     }
     // device memory on one device, or page-locked host memory (zero-copy)
     const size_t src_extent = (nstripes - 1) * sss + (k - 1) * sbs + sz;
