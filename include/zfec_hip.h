@@ -175,6 +175,15 @@ const char* fec_last_kernel_name(void);
  * every mode. */
 int fec_jit_mode(int mode);
 
+/* Wide-code launches that no compiled specialised kernel serves (a decode of
+ * an erasure pattern seen for the first time, small launches, JIT off) run on
+ * matapply_bsg: the same bit-sliced arithmetic with the coefficient matrix as
+ * run-time data (no compile step).  mode 1 = on (default; environment
+ * ZFEC_HIP_GENERIC=0 starts it off), 0 = off (the table-lookup kernels
+ * serve them).  Returns the previous mode; any other value only queries.
+ * Results are bit-identical either way. */
+int fec_generic_mode(int mode);
+
 /* Wait for background compiles; returns the number of compiled kernels. */
 int fec_jit_wait(void);
 

@@ -668,20 +668,24 @@ def test_config2_64mib_vs_oracle():
 class _kernels(object):
     """Which kernel family serves a full-size launch: "jit" = the run-time
     specialised bit-sliced kernel of the launch's matrix (compiled up front with
-    fec_jit_prepare_*, as bench.py times it), "table" = the JIT off (the kernels
-    a launch falls back on).  check(what) asserts the last launch's kernel."""
+    fec_jit_prepare_*, as bench.py times it), "generic" = matapply_bsg (the
+    bit-sliced kernel with the matrix as run-time data: what a first-seen
+    erasure pattern runs on), "table" = the table-lookup kernels (JIT and
+    generic kernel off).  check(what) asserts the last launch's kernel."""
 
-    PREFIX = {"jit": "zfec_hip_bitslice", "table": "matapply_"}
+    PREFIX = {"jit": "zfec_hip_bitslice", "generic": "matapply_bsg", "table": "matapply_lds"}
 
     def __init__(self, kind):
         self.kind = kind
 
     def __enter__(self):
         self.prev = capi.jit_mode(capi.JIT_AUTO if self.kind == "jit" else capi.JIT_OFF)
+        self.prev_g = capi.generic_mode(0 if self.kind == "table" else 1)
         return self
 
     def __exit__(self, *exc):
         capi.jit_mode(self.prev)
+        capi.generic_mode(self.prev_g)
         return False
 
     def prepare(self, code, enc_nums=None, dec_slots=None):
@@ -738,11 +742,11 @@ def _batched_full_size(k, m, S, ns, seed, sample, kernels=None):
         assert (rv == oracle.decode(k, m, recv[s, :, :sz].cpu().numpy(), slots)).all(), s
 
 
-@pytest.mark.parametrize("kind", ["jit", "table"])
+@pytest.mark.parametrize("kind", ["jit", "generic", "table"])
 def test_config4_1024_stripes_of_1mib(kind):
     """cfg4: K=20/M=60, 1024 x 1 MiB stripes in one launch, on the kernel
-    bench.py times (the bit-sliced kernel of the matrix) and on the table
-    kernel."""
+    bench.py times (the bit-sliced kernel of the matrix), on the generic
+    bit-sliced kernel and on the table kernel."""
     with _kernels(kind) as kn:
         _batched_full_size(20, 60, 1 << 20, 1024, 4, sample=6, kernels=kn)
 
@@ -752,13 +756,13 @@ def test_config5_1e6_objects_of_4kib():
     _batched_full_size(3, 10, 4096, 10 ** 6, 5, sample=200)
 
 
-@pytest.mark.parametrize("kind", ["jit", "table"])
+@pytest.mark.parametrize("kind", ["jit", "generic", "table"])
 def test_config3_256mib_roundtrip(kind):
     """K=10/M=16, 256 MiB: encode, drop primaries 0-5, decode; compare by
     equality on the device (size-independent property) and check parity rows
     and recovered blocks against the oracle on slices at the start, middle and
-    end (column independence), on the kernel bench.py times and on the table
-    kernel."""
+    end (column independence), on the kernel bench.py times, on the generic
+    bit-sliced kernel and on the table kernel."""
     k, m, S = 10, 16, 256 << 20
     sz = -(-S // k)
     g = torch.Generator(device="cuda").manual_seed(3)

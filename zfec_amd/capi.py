@@ -45,6 +45,7 @@ SYMBOLS = [
     ("fec_last_kernel_name", ctypes.c_char_p, []),
     ("fec_jit_mode", ctypes.c_int, [ctypes.c_int]),
     ("fec_jit_wait", ctypes.c_int, []),
+    ("fec_generic_mode", ctypes.c_int, [ctypes.c_int]),
     ("fec_jit_prepare_encode", ctypes.c_int, [_P, _UP, _SZ]),
     ("fec_jit_prepare_decode", ctypes.c_int, [_P, _UP, _U]),
 ]
@@ -102,6 +103,12 @@ def last_kernel_name():
 def jit_mode(mode=-1):
     """Set the bit-sliced JIT mode (JIT_OFF / JIT_AUTO / JIT_FORCE); returns the previous one."""
     return lib().fec_jit_mode(mode)
+
+
+def generic_mode(mode=-1):
+    """matapply_bsg (run-time-data bit-sliced kernel) on (1) / off (0) for
+    wide-code launches no JIT kernel serves; returns the previous mode."""
+    return lib().fec_generic_mode(mode)
 
 
 def jit_wait():

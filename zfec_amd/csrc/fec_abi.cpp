@@ -777,6 +777,13 @@ FEC_API int fec_jit_mode(int mode) {
     return prev;
 }
 
+FEC_API int fec_generic_mode(int mode) {
+    const int prev = generic_mode();
+    if (mode == 0 || mode == 1) set_generic_mode(mode);
+    set_status(FEC_OK);
+    return prev;
+}
+
 FEC_API int fec_jit_wait(void) {
     set_status(FEC_OK);
     return jit_wait();

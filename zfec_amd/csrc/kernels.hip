@@ -36,8 +36,10 @@
 
 #include "bitslice.hpp"
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 
 namespace zfec_hip {
@@ -651,6 +653,249 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
 }
 
 // ---------------------------------------------------------------------------
+// matapply_bsg<RT, P>: bit-sliced, with the coefficient matrix as run-time data
+// (no compile step: every erasure pattern runs at this speed the first time).
+//
+// Multiplication by c is an 8x8 GF(2) matrix on the bits of a byte.  After an
+// 8x8 bit transpose a lane's 32 bytes are 8 bit-planes p0..p7, and output
+// plane b of c*x is L[ml_b] ^ H[mh_b], where L[m] is the XOR of the planes
+// {a < 4 : bit a of m} and H[m] that of {4 + a : bit a of m}; ml_b / mh_b are
+// the low / high nibble of the bit-b row of c's matrix (bitslice.cpp's JIT
+// bakes the same choice of combinations into the instruction stream).  Here
+// each input's 15 + 15 combinations go to LDS, and a wave selects them with
+// the nibbles as wave-uniform LDS offsets: per coefficient and output plane two
+// ds_read_b64 (both of the lane's 32-byte groups at once) and one v_bitop3
+// XOR3 per group, against 4.5 VOP3 per 4 bytes for the table kernels.
+//
+// One workgroup (4 waves) per unit of 4 KiB of every block of a stripe: lane l
+// owns bytes 16l + 1024h (h = 0..3) of each block, two 32-byte groups (h = 0,1
+// and h = 2,3).  The r output rows are split over the 4 waves (RT rows each,
+// accumulators in registers).  Inputs go in phases of P: wave w loads input
+// j = P*phase + w, transposes it, and writes its combinations to LDS slot w;
+// after a barrier every wave folds the phase's P inputs into its rows.
+// LDS per slot: 32 combinations x 64 lanes x 8 B = 16 KiB (entries 0 and 16
+// hold zeros, written once).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBsgChunk = 4096;        // bytes of each block per unit
+constexpr uint32_t kBsgSlotBytes = 32 * 512;  // one input's combinations
+
+// g_bsg.off[c]: sixteen dwords, the LDS byte offsets of the combinations
+// output plane b of c*x needs: [b] = L[ml_b], [8 + b] = H[mh_b] (b = 0..7).
+struct BsgBank {
+    uint32_t off[256 * 16];
+};
+
+constexpr BsgBank make_bsg_bank() {
+    BsgBank t{};
+    for (uint32_t c = 0; c < 256; ++c) {
+        uint32_t p[8] = {};
+        p[0] = c;  // c * 2^a
+        for (int a = 1; a < 8; ++a) p[a] = ct_xtime(p[a - 1]);
+        for (uint32_t b = 0; b < 8; ++b) {
+            uint32_t ml = 0, mh = 0;
+            for (uint32_t a = 0; a < 4; ++a) {
+                ml |= ((p[a] >> b) & 1u) << a;
+                mh |= ((p[a + 4] >> b) & 1u) << a;
+            }
+            t.off[c * 16 + b] = ml * 512u;
+            t.off[c * 16 + 8 + b] = (16u + mh) * 512u;
+        }
+    }
+    return t;
+}
+
+__constant__ BsgBank g_bsg = make_bsg_bank();
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(a, b, m, 0xE4);  // m ? a : b, bitwise
+}
+
+// one block swap of the 8x8 bit transpose, four byte lanes at once
+__device__ __forceinline__ void bswap_blocks(uint32_t& a, uint32_t& b, int s, uint32_t m) {
+    const uint32_t t0 = bsel(m, a, b << s);
+    const uint32_t t1 = bsel(m, a >> s, b);
+    a = t0;
+    b = t1;
+}
+
+// 8 dwords (32 bytes) <-> 8 bit-planes; the transpose is its own inverse
+__device__ __forceinline__ void transpose8(uint32_t (&v)[8]) {
+    bswap_blocks(v[0], v[4], 4, 0x0F0F0F0Fu);
+    bswap_blocks(v[1], v[5], 4, 0x0F0F0F0Fu);
+    bswap_blocks(v[2], v[6], 4, 0x0F0F0F0Fu);
+    bswap_blocks(v[3], v[7], 4, 0x0F0F0F0Fu);
+    bswap_blocks(v[0], v[2], 2, 0x33333333u);
+    bswap_blocks(v[1], v[3], 2, 0x33333333u);
+    bswap_blocks(v[4], v[6], 2, 0x33333333u);
+    bswap_blocks(v[5], v[7], 2, 0x33333333u);
+    bswap_blocks(v[0], v[1], 1, 0x55555555u);
+    bswap_blocks(v[2], v[3], 1, 0x55555555u);
+    bswap_blocks(v[4], v[5], 1, 0x55555555u);
+    bswap_blocks(v[6], v[7], 1, 0x55555555u);
+}
+
+// The 15 nonzero combinations of planes q[0..3] of both groups, to LDS
+// entries base + 1..15 (entry e of lane l at e * 512 + l * 8).
+__device__ __forceinline__ void write_combos(char* slot, uint32_t lane8, const uint32_t (&q0)[4],
+                                             const uint32_t (&q1)[4], uint32_t base) {
+    uint32_t c0[16], c1[16];
+    c0[0] = 0u;
+    c1[0] = 0u;
+#pragma unroll
+    for (int m = 1; m < 16; ++m) {
+        const int top = 31 - __builtin_clz(m);
+        c0[m] = c0[m ^ (1 << top)] ^ q0[top];
+        c1[m] = c1[m ^ (1 << top)] ^ q1[top];
+        *reinterpret_cast<u32x2*>(slot + (base + m) * 512u + lane8) = u32x2{c0[m], c1[m]};
+    }
+}
+
+// Rows are interleaved over the waves: wave w owns rows w + 4*rr, rr < RT.
+// launch_bsg lays the coefficients out for this walk: wave w's bytes of phase
+// f are (js, rr) in order, js < P, rr < RT, at byte (w * nphases + f) *
+// bsg_phase_bytes(P, RT) (rows past r and inputs past k get coefficient 0,
+// whose combinations are the zero entries).  A coefficient's eight offset
+// dwords come from g_bsg by scalar loads, issued one step (row) ahead: a wait
+// for a scalar load also drains the wave's LDS reads, so it must come where
+// the wave has none outstanding.
+template <int P, int RT>
+__host__ __device__ constexpr uint32_t bsg_phase_bytes() {
+    return (P * RT + 3) / 4 * 4;
+}
+
+template <int RT, int P, bool SB = true>
+__global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
+    constexpr uint32_t PB = bsg_phase_bytes<P, RT>();
+    constexpr int ND = PB / 4;           // coefficient dwords per wave and phase
+    extern __shared__ char bsg_lds[];    // P slots of kBsgSlotBytes
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane8 = lane * 8u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t k = job.k, r = job.r;
+    const uint32_t nph = (k + P - 1) / P;
+    // zero entries L[0] and H[0] of every slot (never overwritten)
+    for (uint32_t i = threadIdx.x; i < P * 2 * 64; i += 256) {
+        const uint32_t sl = i / 128, e = (i / 64) & 1u, l = i & 63u;
+        *reinterpret_cast<u32x2*>(bsg_lds + sl * kBsgSlotBytes + e * 16u * 512u + l * 8u) = u32x2{0u, 0u};
+    }
+    const KJob kj = kernarg_job();
+    typedef const __attribute__((address_space(4))) uint32_t* KWords;
+    const KWords cw = (KWords)kj->coef + wave * nph * ND;  // this wave's phases
+    const uint64_t sz = job.sz;
+    // byte offset of unit (s, c) in a block of stripe s: the last unit of a
+    // block ends at sz (overlapping its neighbour)
+    auto unit_off = [&](uint32_t su, uint32_t cu) {
+        uint64_t o = static_cast<uint64_t>(cu) * kBsgChunk;
+        return o > sz - kBsgChunk ? sz - kBsgChunk : o;
+    };
+    const bool builder = wave < static_cast<uint32_t>(P);
+    // the input this wave transposes next, loaded one phase ahead (the next
+    // unit's first phase while the current unit's last phase computes), so a
+    // phase never starts waiting on HBM
+    u32x4 xin[4];
+    auto load_input = [&](uint32_t su, uint32_t cu, uint32_t j) {
+        const uint8_t* ip = kj->in[j] + (su * job.in_sstride + unit_off(su, cu) + lane * 16u);
+        xin[0] = load16(ip);
+        xin[1] = load16(ip + 1024);
+        xin[2] = load16(ip + 2048);
+        xin[3] = load16(ip + 3072);
+    };
+    uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
+    if (builder && s < job.nstripes && wave < k) load_input(s, c, wave);
+    while (s < job.nstripes) {
+        uint32_t s2 = s + job.gs_s, c2 = c + job.gs_c;  // this workgroup's next unit
+        if (c2 >= job.cps) {
+            c2 -= job.cps;
+            ++s2;
+        }
+        const uint64_t off = unit_off(s, c);
+        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        uint32_t acc[RT][2][8];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int b = 0; b < 8; ++b) acc[rr][g][b] = 0u;
+        for (uint32_t f = 0; f < nph; ++f) {
+            const uint32_t j0 = f * P;
+            // build: wave w < P owns input j0 + w
+            const uint32_t jb = j0 + wave;
+            if (builder && jb < k) {
+                uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
+                uint32_t g1[8] = {xin[2].x, xin[2].y, xin[2].z, xin[2].w, xin[3].x, xin[3].y, xin[3].z, xin[3].w};
+                transpose8(g0);
+                transpose8(g1);
+                char* slot = bsg_lds + wave * kBsgSlotBytes;
+                const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, l1[4] = {g1[0], g1[1], g1[2], g1[3]};
+                const uint32_t h0[4] = {g0[4], g0[5], g0[6], g0[7]}, h1[4] = {g1[4], g1[5], g1[6], g1[7]};
+                write_combos(slot, lane8, l0, l1, 0u);
+                write_combos(slot, lane8, h0, h1, 16u);
+            }
+            if (builder) {  // prefetch: this unit's next phase, else the next unit's first
+                if (f + 1 < nph) {
+                    if (jb + P < k) load_input(s, c, jb + P);
+                } else if (s2 < job.nstripes && wave < k) {
+                    load_input(s2, c2, wave);
+                }
+            }
+            // this phase's coefficients (scalar loads, waited for before the barrier)
+            uint32_t cwd[ND];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) cwd[d] = cw[f * ND + d];
+            auto coef_at = [&](int t) { return (cwd[t >> 2] >> ((t & 3) * 8)) & 0xFFu; };
+            __syncthreads();
+            const uint32_t jn = k - j0 < static_cast<uint32_t>(P) ? k - j0 : static_cast<uint32_t>(P);
+            uint32_t o[16];
+#pragma unroll
+            for (int b = 0; b < 16; ++b) o[b] = g_bsg.off[coef_at(0) * 16u + b];
+#pragma unroll
+            for (int t = 0; t < P * RT; ++t) {
+                const int js = t / RT, rr = t % RT;
+                if (static_cast<uint32_t>(js) >= jn) break;  // wave-uniform
+                uint32_t on[16];
+                if (t + 1 < P * RT) {  // the next step's offsets, in flight during this step
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) on[b] = g_bsg.off[coef_at(t + 1) * 16u + b];
+                }
+                const char* base = bsg_lds + js * kBsgSlotBytes + lane8;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const u32x2 vl = *reinterpret_cast<const u32x2*>(base + o[b]);
+                    const u32x2 vh = *reinterpret_cast<const u32x2*>(base + o[8 + b]);
+                    acc[rr][0][b] = xor3(acc[rr][0][b], vl.x, vh.x);
+                    acc[rr][1][b] = xor3(acc[rr][1][b], vl.y, vh.y);
+                }
+                // SB: one row's 16 LDS reads in flight at a time (hoisting the
+                // next rows' reads costs registers, i.e. occupancy)
+                if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+                if (t + 1 < P * RT) {
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) o[b] = on[b];
+                }
+            }
+            __syncthreads();  // every wave has read the slots before the next phase overwrites them
+        }
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            const uint32_t i = wave + 4u * rr;
+            if (i >= r) break;  // wave-uniform
+            transpose8(acc[rr][0]);
+            transpose8(acc[rr][1]);
+            uint8_t* op = kj->out[i] + ob;
+            store16_out<true>(op, u32x4{acc[rr][0][0], acc[rr][0][1], acc[rr][0][2], acc[rr][0][3]});
+            store16_out<true>(op + 1024, u32x4{acc[rr][0][4], acc[rr][0][5], acc[rr][0][6], acc[rr][0][7]});
+            store16_out<true>(op + 2048, u32x4{acc[rr][1][0], acc[rr][1][1], acc[rr][1][2], acc[rr][1][3]});
+            store16_out<true>(op + 3072, u32x4{acc[rr][1][4], acc[rr][1][5], acc[rr][1][6], acc[rr][1][7]});
+        }
+        s = s2;
+        c = c2;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Dispatch
 // ---------------------------------------------------------------------------
 typedef void (*KernelFn)(const MatJob);
@@ -765,7 +1010,109 @@ Variant* pick(uint32_t k, uint32_t r, bool acc, uint64_t sz = 0, uint64_t nstrip
 
 thread_local const char* t_last_kernel = "";
 
+// ---- matapply_bsg dispatch ------------------------------------------------------
+// Rows per wave: the smallest instantiated RT >= ceil(r / 4).
+constexpr int kBsgRT[] = {1, 2, 3, 4, 5, 6, 8, 10, 12};
+constexpr int kBsgNumRT = sizeof(kBsgRT) / sizeof(kBsgRT[0]);
+
+struct BsgVariant {
+    KernelFn fn = nullptr;
+    char name[40] = "";
+    int blocks_per_cu = 0;
+    int phase = 4;
+};
+BsgVariant g_bsg_var[3][kBsgNumRT];  // [0: P = 4, 1: P = 2, 2: P = 2 without the per-row sched_barrier][RT index]
+std::once_flag g_bsg_once;
+std::atomic<int> g_generic{-1};
+
+template <int I, int P, bool SB>
+void fill_bsg() {
+    constexpr int RT = kBsgRT[I];
+    BsgVariant& v = g_bsg_var[P == 4 ? 0 : (SB ? 1 : 2)][I];
+    v.fn = matapply_bsg<RT, P, SB>;
+    v.phase = P;
+    snprintf(v.name, sizeof v.name, SB ? "matapply_bsg<%d,%d>" : "matapply_bsg<%d,%d,nosb>", RT, P);
+    if constexpr (I + 1 < kBsgNumRT) fill_bsg<I + 1, P, SB>();
+}
+
+void init_bsg() {
+    fill_bsg<0, 4, true>();
+    fill_bsg<0, 2, true>();
+    fill_bsg<0, 2, false>();
+}
+
+bool bsg_eligible(const MatJob& job) {
+    if (generic_mode() == 0 || job.accumulate || job.tables == 1 || job.sz < kBsgChunk) return false;
+    if (job.k * job.r < 24 || (job.k <= 4 && job.r <= 8)) return false;
+    return job.r <= 4u * static_cast<uint32_t>(kBsgRT[kBsgNumRT - 1]);
+}
+
+hipError_t launch_bsg(MatJob& job, hipStream_t stream) {
+    std::call_once(g_dispatch_once, init_dispatch);
+    std::call_once(g_bsg_once, init_bsg);
+    const uint32_t need_rt = (job.r + 3) / 4;
+    int ri = 0;
+    while (kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
+    // inputs per LDS phase: 2 (default: 32 KiB per workgroup, 4 workgroups per
+    // CU) or 4 (ZFEC_HIP_BSG_PHASE=4, A/B: 64 KiB, 2 per CU)
+    // (ZFEC_HIP_BSG_SB=1, A/B: a scheduling barrier after each row; without
+    // it the compiler overlaps rows and uses fewer registers: cfg4 decode
+    // 1679 -> 1842 GB/s of input, profiles/r02_bsg_ab.log)
+    const char* ph = getenv("ZFEC_HIP_BSG_PHASE");
+    const char* sb = getenv("ZFEC_HIP_BSG_SB");
+    BsgVariant& v = g_bsg_var[(ph && ph[0] == '4') ? 0 : (sb && sb[0] == '1') ? 1 : 2][ri];
+    // coefficients in the kernel's walk order: wave w's bytes of phase f at
+    // (w * nph + f) * PB, (js, rr) in order: row w + 4 * rr of input P * f + js
+    const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = static_cast<uint32_t>(v.phase);
+    const uint32_t PB = (P * RT + 3) / 4 * 4, nph = (job.k + P - 1) / P;
+    if (4u * nph * PB > static_cast<uint32_t>(kMaxCoef)) return hipErrorNotSupported;
+    if (job.tables != 2) {
+        uint8_t cf[kMaxCoef] = {};
+        for (uint32_t w = 0; w < 4; ++w)
+            for (uint32_t f = 0; f < nph; ++f)
+                for (uint32_t js = 0; js < P; ++js)
+                    for (uint32_t rr = 0; rr < RT; ++rr) {
+                        const uint32_t i = w + 4 * rr, j = P * f + js;
+                        cf[(w * nph + f) * PB + js * RT + rr] = i < job.r && j < job.k ? job.coef[i * job.k + j] : 0;
+                    }
+        std::memcpy(job.coef, cf, sizeof cf);
+    }
+    job.tables = 2;  // idempotent: a relaunch of this job keeps the layout
+    const size_t lds = size_t(v.phase) * kBsgSlotBytes;
+    const uint64_t cps = (job.sz + kBsgChunk - 1) / kBsgChunk;
+    const uint64_t units = cps * job.nstripes;
+    if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
+    if (v.blocks_per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v.fn), 256, lds) !=
+                hipSuccess ||
+            nb <= 0)
+            nb = 1;
+        v.blocks_per_cu = nb;
+    }
+    const uint64_t cap = uint64_t(g_num_cu) * v.blocks_per_cu * 8;
+    const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_s = static_cast<uint32_t>(grid / cps);
+    job.gs_c = static_cast<uint32_t>(grid % cps);
+    hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), lds, stream, job);
+    t_last_kernel = v.name;
+    return hipGetLastError();
+}
+
 }  // namespace
+
+int generic_mode() {
+    int g = g_generic.load();
+    if (g < 0) {
+        const char* e = getenv("ZFEC_HIP_GENERIC");
+        g = (e && e[0] == '0') ? 0 : 1;
+        g_generic.store(g);
+    }
+    return g;
+}
+
+void set_generic_mode(int on) { g_generic.store(on ? 1 : 0); }
 
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate) {
     return pick(k, r, accumulate)->name;
@@ -785,6 +1132,10 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
             return hipSuccess;
         }
         if (je != hipErrorNotSupported && je != hipErrorNotReady) return je;
+    }
+    if (bsg_eligible(job)) {
+        const hipError_t be = launch_bsg(job, stream);
+        if (be != hipErrorNotSupported) return be;  // else the table kernels serve
     }
     Variant* v = pick(job.k, job.r, job.accumulate != 0, job.sz, job.nstripes);
     const uint64_t cps = (job.sz + v->chunk - 1) / v->chunk;

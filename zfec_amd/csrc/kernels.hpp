@@ -31,7 +31,8 @@ struct alignas(16) MatJob {
     uint32_t cps;          // 16-byte chunks per stripe = ceil(sz / 16)
     uint32_t gs_c, gs_s;   // grid stride expressed as (chunks, stripes): stride = gs_s*cps + gs_c
     uint32_t accumulate;   // 1: out ^= result (continuation pass for k > kMaxIn)
-    uint32_t tables;       // set by launch_matapply: 1 = tab[] holds the per-coefficient tables
+    uint32_t tables;       // set by launch_matapply: 1 = tab[] holds the per-coefficient tables,
+                           // 2 = coef[] is in matapply_bsg's walk order
     const uint8_t* in[kMaxIn];
     uint8_t* out[kMaxOut];
     union {
@@ -51,8 +52,15 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream);
 // run-time specialised kernel applies (for tests / profiling).
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
 
-// Name of the kernel the calling thread launched last (table variant or
-// bit-sliced JIT kernel, bitslice.hpp).
+// Name of the kernel the calling thread launched last (table variant,
+// run-time-data bit-sliced kernel matapply_bsg, or bit-sliced JIT kernel,
+// bitslice.hpp).
 const char* matapply_last_kernel();
+
+// matapply_bsg (bit-sliced, coefficients as run-time data) for wide-code
+// launches that no specialised JIT kernel serves: 1 = on (default; env
+// ZFEC_HIP_GENERIC=0 starts it off), 0 = off (the table kernels serve).
+int generic_mode();
+void set_generic_mode(int on);
 
 }  // namespace zfec_hip
