@@ -77,6 +77,11 @@ def parse():
     p.add_argument("--slabs", action="store_true",
                    help="cfg2/cfg3 only: split the ONE stripe's block byte range into slabs across the GPUs "
                         "(zfec_amd.shard.slab_range; strong scaling) instead of one stripe per GPU")
+    p.add_argument("--fresh", type=int, default=None,
+                   help="decodes from fresh random erasure patterns to time (default: 20 for the wide codes cfg3/cfg4, "
+                        "0 otherwise)")
+    p.add_argument("--legs-out", default=None,
+                   help="write the run's launch sequence per leg (JSON) for tools/trace_legs.py")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -190,59 +195,101 @@ def valu_roofline(workload, kernel, launch_ms):
     return None
 
 
+def host_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU
+    quota when one is set (cpu.max), plus what the host reports."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return {"usable": usable, "affinity": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(),
+            "model": model}
+
+
 def cpu_baseline(seconds, k, m, sz):
-    """Bounded CPU sample of the same workload (encode + last-k decode
-    of one stripe of k*sz bytes per step, decoding from the last k blocks), one
-    stripe per thread."""
+    """Bounded CPU sample of the same workload (encode + last-k decode of one
+    stripe of k*sz bytes per step, decoding from the last k blocks), one
+    stripe per thread on every CPU this process may use (no cap), plus a
+    1-thread figure.  Stripes are shrunk so all threads' buffers stay within
+    ~8 GB of host memory."""
     from oracle import oracle
 
     ref = oracle.ref_module()
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(16, threads))
+    cpus = host_cpus()
+    threads = cpus["usable"]
+    sz = max(1, min(sz, (8 << 30) // (threads * (m + k))))
     rng = np.random.default_rng(7)
     proto = [rng.integers(0, 256, size=sz, dtype=np.uint8).tobytes() for _ in range(k)]
-    counts = [0] * threads
-    stop = threading.Event()
     nums = place(list(range(m - k, m)), k)  # the same last-k decode set as the GPU leg
     if ref is not None:
         kind = "reference"
 
-        def work(t):
-            enc, dec = ref.Encoder(k, m), ref.Decoder(k, m)
-            blocks = [bytes(b) for b in proto]
-            while not stop.is_set():
-                out = enc.encode(blocks)
-                dec.decode([out[n] for n in nums], nums)
-                counts[t] += 1
+        def make_work(counts, stop):
+            def work(t):
+                enc, dec = ref.Encoder(k, m), ref.Decoder(k, m)
+                blocks = [bytes(b) for b in proto]
+                while not stop.is_set():
+                    out = enc.encode(blocks)
+                    dec.decode([out[n] for n in nums], nums)
+                    counts[t] += 1
+            return work
     else:
         kind = "port"
         data = np.frombuffer(b"".join(proto), dtype=np.uint8).reshape(k, sz)
 
-        def work(t):
-            while not stop.is_set():
-                allb = np.concatenate([data, oracle.encode(k, m, data)])
-                oracle.decode(k, m, allb[nums], nums)
-                counts[t] += 1
+        def make_work(counts, stop):
+            def work(t):
+                while not stop.is_set():
+                    allb = np.concatenate([data, oracle.encode(k, m, data)])
+                    oracle.decode(k, m, allb[nums], nums)
+                    counts[t] += 1
+            return work
 
-    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
-    t0 = time.perf_counter()
-    for th in ths:
-        th.start()
-    time.sleep(seconds)
-    stop.set()
-    for th in ths:
-        th.join()
-    el = time.perf_counter() - t0  # threads finish their step in flight; all of it is counted
-    steps = sum(counts)
+    def run(nthreads, secs):
+        counts = [0] * nthreads
+        stop = threading.Event()
+        work = make_work(counts, stop)
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(nthreads)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        time.sleep(secs)
+        stop.set()
+        for th in ths:
+            th.join()
+        el = time.perf_counter() - t0  # threads finish their step in flight; all of it is counted
+        return sum(counts), el
+
+    steps1, el1 = run(1, max(2.0, seconds * 0.3))
+    steps, el = run(threads, seconds)
+    src = ("reference zfec/fec.c+_fecmodule.c compiled by oracle/Makefile (-O2 -march=x86-64-v2)"
+           if kind == "reference" else "oracle/fec_oracle.c restatement")
     return {"value": round(steps * 2 * k * sz / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": kind,
-            "sample": "%d steps (encode + last-k decode of a K=%d/M=%d %d-byte stripe) in %.1f s, one "
-                      "stripe per thread; %s" % (
-                          steps, k, m, k * sz, el,
-                          "reference zfec/fec.c+_fecmodule.c compiled by oracle/Makefile (-O2 -march=x86-64-v2)"
-                          if kind == "reference" else "oracle/fec_oracle.c restatement")}
+            "value_1thread": round(steps1 * 2 * k * sz / el1 / 1e9, 4),
+            "host": cpus,
+            "sample": "%d steps (encode + last-k decode of a K=%d/M=%d %d-byte stripe) in %.1f s on %d threads, "
+                      "one stripe per thread, every CPU the process may use (affinity %d, cgroup quota %s, "
+                      "os.cpu_count %s); 1 thread: %d steps in %.1f s; %s" % (
+                          steps, k, m, k * sz, el, threads, cpus["affinity"], cpus["cgroup_quota_cpus"],
+                          cpus["os_cpu_count"], steps1, el1, src)}
 
 
 def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
@@ -274,7 +321,55 @@ def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
     return {key: round(v, 1) for key, v in res.items()}
 
 
-def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True):
+class Legs(object):
+    """Order of this process's library launches, run-length encoded per leg,
+    so tools/trace_legs.py can split a rocprofv3 kernel trace of this run into
+    the same legs (the dispatches of the zfec kernels, in order)."""
+
+    def __init__(self):
+        self.runs = []
+
+    def add(self, leg, kernel):
+        if self.runs and self.runs[-1][0] == leg and self.runs[-1][1] == kernel:
+            self.runs[-1][2] += 1
+        else:
+            self.runs.append([leg, kernel, 1])
+
+
+LEGS = Legs()
+
+# the 256 MiB Infinity Cache (MALL): buffer rotations for cold launches span
+# at least this many bytes, so a launch's buffers were last touched >= 2 x the
+# cache's size of traffic ago
+COLD_SPAN = 768 << 20
+
+
+def back_to_back(fns, n, stream, leg):
+    """Average GPU duration of n launches queued back to back, fns[i % len]
+    for launch i.  The stream is held by a spin kernel while the host enqueues
+    them, so the host's per-call cost cannot leave gaps between the timed
+    launches.  Returns (ms per launch, host enqueue us per launch)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fns[0](stream.cuda_stream)
+    LEGS.add(leg + " (untimed)", capi.last_kernel_name())
+    torch.cuda._sleep(20_000_000)
+    for i in range(3):  # queued behind the spin kernel too: the timed launches start on a busy GPU
+        fns[(i + 1) % len(fns)](stream.cuda_stream)
+        LEGS.add(leg + " (untimed)", capi.last_kernel_name())
+    a.record(stream)
+    h0 = time.perf_counter()
+    for i in range(n):
+        fns[(i + 4) % len(fns)](stream.cuda_stream)
+    host_us = (time.perf_counter() - h0) / n * 1e6
+    b.record(stream)
+    kern = capi.last_kernel_name()
+    for _ in range(n):
+        LEGS.add(leg, kern)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n, host_us
+
+
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True, fresh=0):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
@@ -282,52 +377,70 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
     reference's API takes separate buffers per block, which are aligned too).
     row_padding: the calls carry FEC_FLAG_ROW_PADDING, letting the library run
     each row out to its next 128-byte line inside that padding (whole-line
-    writes; the bytes counted stay k*sz per stripe)."""
+    writes; the bytes counted stay k*sz per stripe).
+    fresh: that many extra decodes, each from a new random set of k received
+    blocks (a matrix never seen before: no specialised kernel exists for it)."""
     r = m - k
     ld = row_stride(sz, layout)
     gen = torch.Generator(device="cuda").manual_seed(1234 + k)
-    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen)
-    par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
     # decode from the last k blocks (all secondaries when m >= 2k); primaries at their slot
     slots = place(list(range(m - k, m)), k)
     nrec = sum(1 for s in slots if s >= k)
-    recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")  # received blocks, slot order
-    rec = torch.empty((ns, nrec, ld), dtype=torch.uint8, device="cuda")
+    # rotation sets for the cold legs: set 0 is the timed loop's
+    enc_fp, dec_fp = (k + r) * ld * ns, (k + nrec) * ld * ns
+    nsets = max(2, -(-COLD_SPAN // min(enc_fp, dec_fp)))
+    data = [torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen) for _ in range(nsets)]
+    par = [torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+    recv = [torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda") for _ in range(nsets)]  # slot order
+    rec = [torch.empty((ns, nrec, ld), dtype=torch.uint8, device="cuda") for _ in range(nsets)]
     enc_nums = list(range(k, m))
     code = capi.Code(k, m)
     fl = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if row_padding else 0)
 
-    def enc(sh):
-        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, enc_nums, sz, ns, stream=sh,
-                          flags=fl)
+    def enc_i(i):
+        def f(sh):
+            code.encode_batch(data[i].data_ptr(), ld, k * ld, par[i].data_ptr(), ld, r * ld, enc_nums, sz, ns,
+                              stream=sh, flags=fl)
+        return f
 
-    def dec(sh):
-        code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, nrec * ld, slots, sz, ns, stream=sh,
-                          flags=fl)
+    def dec_i(i):
+        def f(sh):
+            code.decode_batch(recv[i].data_ptr(), ld, k * ld, rec[i].data_ptr(), ld, nrec * ld, slots, sz, ns,
+                              stream=sh, flags=fl)
+        return f
 
+    enc, dec = enc_i(0), dec_i(0)
     stream = torch.cuda.current_stream()
-    enc(stream.cuda_stream)
-    for i, s in enumerate(slots):  # stage the received blocks once (not part of a step)
-        recv[:, i].copy_(data[:, s] if s < k else par[:, s - k])
-    dec(stream.cuda_stream)
+    for i in range(nsets):
+        enc_i(i)(stream.cuda_stream)
+        LEGS.add("setup", capi.last_kernel_name())
+        for j, s in enumerate(slots):  # stage the received blocks once (not part of a step)
+            recv[i][:, j].copy_(data[i][:, s] if s < k else par[i][:, s - k])
+        dec_i(i)(stream.cuda_stream)
+        LEGS.add("setup", capi.last_kernel_name())
     # wide codes: a matrix's second large launch queues the background compile
     # of its bit-sliced kernel (zfec_amd/csrc/bitslice.cpp); wait for it so the
     # warmup and the timed loop run the kernels a long-running user gets
-    enc(stream.cuda_stream)
-    dec(stream.cuda_stream)
     capi.jit_wait()
     kernels = {}
     for i in range(max(1, warmup)):
         enc(stream.cuda_stream)
         kernels["encode"] = capi.last_kernel_name()
+        LEGS.add("warmup", kernels["encode"])
         dec(stream.cuda_stream)
         kernels["decode"] = capi.last_kernel_name()
+        LEGS.add("warmup", kernels["decode"])
     torch.cuda.synchronize()
     missing = [i for i in range(k) if slots[i] >= k]
-    assert torch.equal(rec[:, :, :sz], data[:, missing, :sz]), "decode(encode(x)) != x"
+    for i in range(nsets):
+        assert torch.equal(rec[i][:, :, :sz], data[i][:, missing, :sz]), "decode(encode(x)) != x"
 
     launch = "eager"
-    step = lambda: (enc(stream.cuda_stream), dec(stream.cuda_stream))
+
+    def step():
+        enc(stream.cuda_stream)
+        dec(stream.cuda_stream)
+
     if use_graph:
         try:
             cap = torch.cuda.Stream()
@@ -337,16 +450,19 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
                 enc(cap.cuda_stream)
                 dec(cap.cuda_stream)
             torch.cuda.synchronize()
-            rec.zero_()
+            rec[0].zero_()
             graph.replay()
             torch.cuda.synchronize()
-            assert torch.equal(rec[:, :, :sz], data[:, missing, :sz]), "graph replay: decode(encode(x)) != x"
+            assert torch.equal(rec[0][:, :, :sz], data[0][:, missing, :sz]), "graph replay: decode(encode(x)) != x"
             step = graph.replay
             launch = "hipGraph (1 replay per step)"
         except Exception as e:  # capture unsupported: keep eager launches
             launch = "eager (graph capture failed: %s: %s)" % (type(e).__name__, str(e)[:120])
     for _ in range(3):
         step()
+        if launch == "eager":
+            LEGS.add("warmup", kernels["encode"])
+            LEGS.add("warmup", kernels["decode"])
     torch.cuda.synchronize()
     barrier(dist)
     torch.cuda.synchronize()
@@ -359,32 +475,25 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
     torch.cuda.synchronize()
     barrier(dist)
     el = time.perf_counter() - t0
+    if launch == "eager":
+        for _ in range(steps):
+            LEGS.add("timed loop", kernels["encode"])
+            LEGS.add("timed loop", kernels["decode"])
 
-    # Per-kernel launch duration for the roofline: `steps` back-to-back
-    # launches of one kernel between two HIP events on the launch stream
-    # (average duration, launch gaps included; what rocprof's kernel trace
-    # averages plus the gaps).  The interleaved per-launch event pairs of the
-    # timed loop's pattern are reported too (each interval also carries an
-    # event record).
-    def back_to_back(fn, n):
-        """Average GPU duration of n launches queued back to back.  The stream
-        is held by a spin kernel while the host enqueues them, so the host's
-        per-call cost cannot leave gaps between the timed launches."""
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        fn(stream.cuda_stream)
-        torch.cuda._sleep(20_000_000)
-        for _ in range(3):  # queued behind the spin kernel too: the timed launches start on a busy GPU
-            fn(stream.cuda_stream)
-        a.record(stream)
-        h0 = time.perf_counter()
-        for _ in range(n):
-            fn(stream.cuda_stream)
-        host_us = (time.perf_counter() - h0) / n * 1e6
-        b.record(stream)
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / n, host_us
+    # Per-kernel launch duration for the rooflines: back-to-back launches of
+    # one kernel between two HIP events on the launch stream, (a) "warm": the
+    # same buffers every launch (what the timed loop does; footprints under
+    # 256 MiB are then partly served by the Infinity Cache), (b) "cold": a
+    # rotation of `nsets` disjoint buffer sets spanning >= 768 MiB, so every
+    # launch reads and writes HBM.  (c) The timed loop's encode/decode pattern
+    # with an event pair around every launch (each event adds ~1 us).
+    nb = max(20, steps)
+    enc_w, enc_host_us = back_to_back([enc], nb, stream, "encode warm")
+    dec_w, dec_host_us = back_to_back([dec], nb, stream, "decode warm")
+    enc_c, _ = back_to_back([enc_i(i) for i in range(nsets)], nb, stream, "encode cold")
+    dec_c, _ = back_to_back([dec_i(i) for i in range(nsets)], nb, stream, "decode cold")
 
-    def per_launch(n=50):
+    def per_launch(n):
         E = lambda: torch.cuda.Event(enable_timing=True)
         ev = [(E(), E(), E()) for _ in range(n)]
         for a, b, c in ev:
@@ -393,54 +502,117 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
             b.record(stream)
             dec(stream.cuda_stream)
             c.record(stream)
+            LEGS.add("event pairs", kernels["encode"])
+            LEGS.add("event pairs", kernels["decode"])
         torch.cuda.synchronize()
         return (float(np.mean([a.elapsed_time(b) for a, b, _ in ev])),
                 float(np.mean([b.elapsed_time(c) for _, b, c in ev])))
 
-    # The roofline's launch duration: `nb` launches of the kernel back to back
-    # between two HIP events on the launch stream, queued behind 3 untimed
-    # ones; average per launch.  For comparison, the timed loop's
-    # encode/decode pattern with an event pair around every launch (each event
-    # adds ~1 us).
-    nb = max(20, steps)
-    (enc_b2b, enc_host_us), (dec_b2b, dec_host_us) = back_to_back(enc, nb), back_to_back(dec, nb)
     npl = max(50, steps)
     enc_pl, dec_pl = per_launch(npl)
-    return {"elapsed_s": el, "gpu_step_ms": e0.elapsed_time(e1) / steps, "launch": launch,
-            "enc_ms": enc_b2b, "dec_ms": dec_b2b, "enc_ms_pairs": enc_pl, "dec_ms_pairs": dec_pl, "b2b_launches": nb,
-            "enqueue_us": (enc_host_us, dec_host_us),
-            "pair_launches": npl, "nrec": nrec, "slots": slots, "kernels": kernels}
+    out = {"elapsed_s": el, "gpu_step_ms": e0.elapsed_time(e1) / steps, "launch": launch,
+           "enc_ms": enc_c, "dec_ms": dec_c, "enc_ms_warm": enc_w, "dec_ms_warm": dec_w,
+           "enc_ms_pairs": enc_pl, "dec_ms_pairs": dec_pl, "b2b_launches": nb, "nsets": nsets,
+           "enqueue_us": (enc_host_us, dec_host_us),
+           "pair_launches": npl, "nrec": nrec, "slots": slots, "kernels": kernels}
+    if fresh:
+        out["decode_fresh"] = decode_fresh(code, k, m, sz, ns, ld, data[0], par[0], recv[0], fresh, stream)
+    return out
+
+
+def decode_fresh(code, k, m, sz, ns, ld, data, par, recv, n, stream):
+    """Decodes that each use a new random set of k received blocks: a matrix
+    the process has never seen, so no specialised (JIT) kernel exists for it
+    and the launch runs on what serves first-seen patterns (matapply_bsg).
+    One launch per pattern between events (the staging copy into slot order is
+    outside them); every result is checked against the stripe."""
+    rng = np.random.default_rng(4321)
+    out = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
+    rows = []
+    for _ in range(n):
+        while True:
+            nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+            sl = place(nums, k)
+            miss = [i for i in range(k) if sl[i] >= k]
+            if miss:
+                break
+        for j, s in enumerate(sl):
+            recv[:, j].copy_(data[:, s] if s < k else par[:, s - k])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        code.decode_batch(recv.data_ptr(), ld, k * ld, out.data_ptr(), ld, k * ld, sl, sz, ns,
+                          stream=stream.cuda_stream)
+        b.record(stream)
+        kern = capi.last_kernel_name()
+        LEGS.add("decode fresh", kern)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :len(miss), :sz], data[:, miss, :sz]), "fresh-pattern decode != input"
+        ms = a.elapsed_time(b)
+        rows.append((ms, len(miss), kern))
+    gb = [k * sz * ns / (ms * 1e-3) / 1e9 for ms, _, _ in rows]
+    hbm = [(k + nr) * sz * ns / (ms * 1e-3) / 1e9 for ms, nr, _ in rows]
+    return {"patterns": n, "input_GBps_mean": round(float(np.mean(gb)), 1),
+            "input_GBps_min": round(float(np.min(gb)), 1), "hbm_GBps_mean": round(float(np.mean(hbm)), 1),
+            "recovered_mean": round(float(np.mean([nr for _, nr, _ in rows])), 2),
+            "ms_mean": round(float(np.mean([ms for ms, _, _ in rows])), 4),
+            "kernels": sorted(set(kk for _, _, kk in rows)),
+            "timing": "one decode launch per pattern between HIP events; no JIT warm-up (JIT mode as shipped: a "
+                      "pattern's first launch never runs a specialised kernel)"}
 
 
 def run_batched_1mib(steps):
     """North-star shape: K=3/M=10 encode of 1 MiB stripes, 256 stripes per
-    launch (block rows 256-byte aligned, as in the main workload)."""
+    launch, in two layouts:
+      object-major  [stripe][block][row] (rows 256-byte aligned, as in the main
+                    workload): one launch walks 256 stripes of 10 rows each;
+      block-major   block j of every stripe back to back ([block][stripe][sz],
+                    stripe stride = sz): fec_encode_batch runs it as ONE stripe
+                    of 256 x sz bytes per block, 10 long streams.
+    Each is timed back to back on the same buffers ("warm") and over a
+    rotation of disjoint buffer sets spanning >= 768 MiB ("cold": HBM, not the
+    Infinity Cache).  The top-level figures are object-major cold; the
+    layouts' own figures are under "layouts"."""
     k, m, ns = 3, 10, 256
     sz = -(-(1 << 20) // k)
     ld = row_stride(sz)
     code = capi.Code(k, m)
-    src = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda")
-    dst = torch.empty((ns, m - k, ld), dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     nums = list(range(k, m))
+    res = {"shape": "K=3/M=10 encode, 256 x 1 MiB stripes per launch", "algorithmic_bytes_per_launch": m * sz * ns,
+           "layouts": {}}
+    for layout in ("object-major", "block-major"):
+        if layout == "object-major":
+            fp = m * ld * ns
+            shape_in, shape_out = (ns, k, ld), (ns, m - k, ld)
+            sbs, sss, dbs, dss = ld, k * ld, ld, (m - k) * ld
+        else:
+            fp = m * sz * ns
+            shape_in, shape_out = (k, ns * sz), (m - k, ns * sz)
+            sbs, sss, dbs, dss = ns * sz, sz, ns * sz, sz
+        nsets = max(2, -(-COLD_SPAN // fp))
+        src = [torch.randint(0, 256, shape_in, dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+        dst = [torch.empty(shape_out, dtype=torch.uint8, device="cuda") for _ in range(nsets)]
 
-    def enc():
-        code.encode_batch(src.data_ptr(), ld, k * ld, dst.data_ptr(), ld, (m - k) * ld, nums, sz, ns,
-                          stream=st.cuda_stream)
+        def enc_i(i):
+            def f(sh):
+                code.encode_batch(src[i].data_ptr(), sbs, sss, dst[i].data_ptr(), dbs, dss, nums, sz, ns, stream=sh)
+            return f
 
-    for _ in range(3):
-        enc()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(steps):
-        enc()
-    e1.record(st)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    in_gbps = ns * k * sz / (ms * 1e-3) / 1e9
-    hbm = in_gbps * m / k
-    return {"shape": "K=3/M=10 encode, 256 x 1 MiB stripes per launch", "input_GBps": round(in_gbps, 1),
-            "hbm_GBps": round(hbm, 1), "frac_of_peak": round(hbm / HBM_PEAK_GBPS, 4), "ms_per_launch": round(ms, 4)}
+        warm, _ = back_to_back([enc_i(0)], steps, st, "batched_1MiB %s warm" % layout)
+        cold, _ = back_to_back([enc_i(i) for i in range(nsets)], steps, st, "batched_1MiB %s cold" % layout)
+        lr = {"kernel": capi.last_kernel_name(), "nsets": nsets}
+        for tag, ms in (("", cold), ("_warm", warm)):
+            in_gbps = ns * k * sz / (ms * 1e-3) / 1e9
+            hbm = in_gbps * m / k
+            lr.update({"input_GBps" + tag: round(in_gbps, 1), "hbm_GBps" + tag: round(hbm, 1),
+                       "frac_of_peak" + tag: round(hbm / HBM_PEAK_GBPS, 4), "ms_per_launch" + tag: round(ms, 4)})
+        res["layouts"][layout] = lr
+        del src, dst
+        torch.cuda.empty_cache()
+    om = res["layouts"]["object-major"]
+    res.update({key: om[key] for key in ("kernel", "input_GBps", "hbm_GBps", "frac_of_peak", "ms_per_launch",
+                                         "frac_of_peak_warm")})
+    return res
 
 
 def main():
@@ -461,22 +633,29 @@ def main():
         ns = s1 - s0
     else:
         ns = nstripes
+    fresh = args.fresh if args.fresh is not None else (20 if args.workload in ("cfg3", "cfg4") else 0)
     t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout,
-                     row_padding=not args.no_row_padding)
+                     row_padding=not args.no_row_padding, fresh=fresh if rank == 0 else 0)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
     value = total_bytes / el / 1e9
     nrec = t["nrec"]
     enc_bytes = (k + r) * sz * ns    # read k blocks, write m-k blocks, per stripe
     dec_bytes = (k + nrec) * sz * ns  # read k blocks, write the recovered ones
-    enc_ach = enc_bytes / (t["enc_ms"] * 1e-3) / 1e9
-    dec_ach = dec_bytes / (t["dec_ms"] * 1e-3) / 1e9
+    gbps = lambda nbytes, ms: nbytes / (ms * 1e-3) / 1e9
     desc = {"cfg2": "K=3 M=10, one 64 MiB stripe per GPU",
             "cfg3": "K=10 M=16, one 256 MiB stripe per GPU",
             "cfg4": "K=20 M=60, 1 GiB = 1024 x 1 MiB stripes split across GPUs",
             "cfg5": "K=3 M=10, 1e6 x 4 KiB objects split across GPUs"}[args.workload]
     if args.slabs:
         desc = desc.replace("stripe per GPU", "stripe split into byte-range slabs across GPUs")
+    row_padding = not args.no_row_padding
+    timing = ("%d launches back to back between two HIP events on the launch stream, enqueued (after 4 untimed "
+              "ones) while a spin kernel holds the stream (average launch duration, no host gaps), over a rotation "
+              "of %d disjoint buffer sets spanning >= 768 MiB (3x the 256 MiB Infinity Cache), so every launch "
+              "reads and writes HBM; *_warm: the same on one buffer set (as the timed loop runs); "
+              "launch_ms_event_pairs: mean of %d encode/decode steps as in the timed loop with a HIP event pair "
+              "around each launch" % (t["b2b_launches"], t["nsets"], t["pair_launches"]))
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -493,31 +672,43 @@ def main():
         "config": {"workload": "%s: encode (%d->%d blocks) + decode from blocks %s" % (desc, k, r, t["slots"]),
                    "name": args.workload, "k": k, "m": m, "stripe_bytes": stripe, "stripes_per_gpu": ns,
                    "block_bytes": sz_block, "slab_bytes_rank0": sz if args.slabs else None,
-                   "block_row_stride": row_stride(sz, args.layout), "row_padding": not args.no_row_padding,
+                   "block_row_stride": row_stride(sz, args.layout), "row_padding": row_padding,
+                   "value_counts": "input bytes of both directions per step: the encode reads k*sz and the decode "
+                                   "reads k*sz per stripe, so value = 2 x stripe_roundtrip_GBps",
+                   "row_padding_contract": ("FEC_FLAG_ROW_PADDING: the caller's block rows have slack up to the next "
+                                            "128-byte line (row stride %d >= roundup(sz, 128)); the library may "
+                                            "read and write it" % row_stride(sz, args.layout)) if row_padding
+                   else "off: rows end at sz",
                    "parallelism": ("block byte range split into %d slabs (%d B on rank 0), one per GPU, no collective"
                                    % (world, sz) if args.slabs else
                                    "stripes sharded across %d GPU(s), no collective" % world)},
-        "roofline": {"bound": "hbm", "achieved": round(enc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(enc_ach / HBM_PEAK_GBPS, 4), "traffic": None if args.slabs else pmc_traffic(args.workload),
+        "stripe_roundtrip_GBps": round(value / 2, 2),
+        "roofline": {"bound": "hbm", "achieved": round(gbps(enc_bytes, t["enc_ms"]), 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(gbps(enc_bytes, t["enc_ms"]) / HBM_PEAK_GBPS, 4),
+                     "traffic": None if args.slabs else pmc_traffic(args.workload),
                      "kernel": "%s (encode)" % t["kernels"]["encode"], "algorithmic_bytes_per_launch": enc_bytes,
                      "launch_ms": round(t["enc_ms"], 4),
+                     "achieved_warm": round(gbps(enc_bytes, t["enc_ms_warm"]), 1),
+                     "frac_warm": round(gbps(enc_bytes, t["enc_ms_warm"]) / HBM_PEAK_GBPS, 4),
+                     "launch_ms_warm": round(t["enc_ms_warm"], 4),
                      "launch_ms_event_pairs": round(t["enc_ms_pairs"], 4),
                      "host_enqueue_us": round(t["enqueue_us"][0], 1),
-                     "timing": "%d encode launches back to back between two HIP events on the launch stream, "
-                               "enqueued (after 3 untimed ones) while a spin kernel holds the stream (average launch "
-                               "duration, no host gaps); launch_ms_event_pairs: "
-                               "mean of %d encode/decode steps as in the timed loop with a HIP event pair around "
-                               "each launch" % (t["b2b_launches"], t["pair_launches"])},
-        "decode_roofline": {"achieved": round(dec_ach, 1), "frac": round(dec_ach / HBM_PEAK_GBPS, 4),
+                     "timing": timing},
+        "decode_roofline": {"achieved": round(gbps(dec_bytes, t["dec_ms"]), 1),
+                            "frac": round(gbps(dec_bytes, t["dec_ms"]) / HBM_PEAK_GBPS, 4),
                             "kernel": "%s (decode)" % t["kernels"]["decode"],
                             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4),
+                            "frac_warm": round(gbps(dec_bytes, t["dec_ms_warm"]) / HBM_PEAK_GBPS, 4),
+                            "launch_ms_warm": round(t["dec_ms_warm"], 4),
                             "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4)},
         "valu_roofline": None if args.slabs else valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
-        "encode_input_GBps": round(k * sz * ns / (t["enc_ms"] * 1e-3) / 1e9, 1),
-        "decode_input_GBps": round(k * sz * ns / (t["dec_ms"] * 1e-3) / 1e9, 1),
+        "encode_input_GBps": round(gbps(k * sz * ns, t["enc_ms"]), 1),
+        "decode_input_GBps": round(gbps(k * sz * ns, t["dec_ms"]), 1),
     }
+    if "decode_fresh" in t:
+        out["decode_fresh_pattern"] = t["decode_fresh"]
     if rank == 0 and not args.no_extra and args.workload == "cfg2":
         out["batched_1MiB"] = run_batched_1mib(20)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -542,6 +733,9 @@ def main():
             except Exception as e:
                 out["cpu_baseline"]["bench_zfec"] = {"error": repr(e)}
     if rank == 0:
+        if args.legs_out:
+            with open(args.legs_out, "w") as f:
+                json.dump({"workload": args.workload, "legs": LEGS.runs}, f)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

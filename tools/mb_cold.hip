@@ -1,0 +1,242 @@
+// mb_cold.hip -- HBM ceilings of the K=3/M=10 encode's memory pattern from
+// cold caches: 256 stripes x 1 MiB (bench.py's batched_1MiB layout,
+// [stripe][block][row], rows of 349,696 bytes), launches rotated over buffer
+// sets spanning > 768 MiB so no launch finds its bytes in the 256 MiB
+// Infinity Cache.  Every variant moves the same bytes: 3 x 16-byte loads and
+// 7 x 16-byte stores per lane per unit; the arithmetic is an XOR (a copy
+// ceiling), except "prod", which is the production dispatcher's kernel.
+//
+// Walk variants:
+//   lane     one 16-byte unit per lane, grid = units / 256 (production walk)
+//   persist  persistent grid (CUs x 8 workgroups), grid-stride over units
+//   xcd      as `lane`, but workgroups dealt so that the 8 XCDs (blockIdx % 8)
+//            each sweep one contiguous eighth of the units
+//   wave4    each wave owns 4 consecutive 1 KiB pieces of every block
+//            (4 KiB contiguous per block per wave), lanes 1 KiB apart
+//   plain    `lane` with default-policy stores instead of nt
+//   ntload   `lane` with nt loads too
+//   prod / prod_xcd: the production kernel without / with XCD-contiguous
+//            workgroup order (ZFEC_HIP_XCD)
+//   prod_gmN the production kernel with its grid capped at N x the resident
+//            workgroups (a grid-stride walk of ~units / (N x resident lanes)
+//            units per lane; the default cap is 1024, i.e. one unit per lane)
+//   prod_bm  the production kernel on the same stripes stored block-major
+//            (one long row per block, as fec_encode_batch collapses them)
+// usage: tools/mb_cold.exe [buffer sets] [stripes]
+// Ceilings: read3 (only the 3 loads), write7 (only the 7 stores), copy1
+// (1 load, 1 store per unit).
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_cold.hip zfec_amd/csrc/bitslice.cpp \
+//          zfec_amd/csrc/gf256.cpp -ldl -o tools/mb_cold.exe
+#include "../zfec_amd/csrc/kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace zfec_hip;
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+namespace {
+
+constexpr int K = 3, R = 7;
+
+struct Lay {
+    uint8_t* in;
+    uint8_t* out;
+    uint64_t ld;       // row bytes
+    uint32_t cps;      // 16-byte chunks per row
+    uint32_t units;    // cps * nstripes
+};
+
+__device__ __forceinline__ void unit_io(const Lay& L, uint32_t u, bool ntload, bool ntstore, int mode) {
+    const uint32_t s = u / L.cps, c = u - s * L.cps;
+    const uint64_t ib = uint64_t(s) * K * L.ld + uint64_t(c) * 16;
+    const uint64_t ob = uint64_t(s) * R * L.ld + uint64_t(c) * 16;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    if (mode != 2) {  // loads
+        const int nl = mode == 3 ? 1 : K;
+        for (int j = 0; j < nl; ++j) {
+            const u32x4* p = reinterpret_cast<const u32x4*>(L.in + ib + j * L.ld);
+            acc ^= ntload ? __builtin_nontemporal_load(p) : *p;
+        }
+    } else {
+        acc = u32x4{u, u + 1, u + 2, u + 3};
+    }
+    if (mode == 1) {  // read only: keep the loads alive
+        if (acc.x == 0x12345678u && acc.y == 0x9abcdef0u) *reinterpret_cast<u32x4*>(L.out + ob) = acc;
+        return;
+    }
+    const int ns = mode == 3 ? 1 : R;
+    for (int r = 0; r < ns; ++r) {
+        u32x4* q = reinterpret_cast<u32x4*>(L.out + ob + r * L.ld);
+        if (ntstore)
+            __builtin_nontemporal_store(acc ^ uint32_t(r), q);
+        else
+            *q = acc ^ uint32_t(r);
+    }
+}
+
+// walk: 0 lane, 1 persist, 2 xcd, 3 wave4.  mode: 0 encode-shaped, 1 read3, 2 write7, 3 copy1
+template <int WALK, bool NTL, bool NTS, int MODE>
+__global__ __launch_bounds__(256) void mb(const Lay L) {
+    if constexpr (WALK == 0) {
+        const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+        if (u < L.units) unit_io(L, u, NTL, NTS, MODE);
+    } else if constexpr (WALK == 1) {
+        for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < L.units; u += gridDim.x * 256)
+            unit_io(L, u, NTL, NTS, MODE);
+    } else if constexpr (WALK == 2) {
+        const uint32_t nwg = gridDim.x, q = nwg / 8, rr = nwg % 8, x = blockIdx.x % 8;
+        const uint32_t wg = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + blockIdx.x / 8;
+        const uint32_t u = wg * 256 + threadIdx.x;
+        if (u < L.units) unit_io(L, u, NTL, NTS, MODE);
+    } else {
+        // wave w of the grid owns 64-lane pieces 4w..4w+3 of the unit sequence
+        const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t u = (wave * 4 + p) * 64 + lane;
+            if (u < L.units) unit_io(L, u, NTL, NTS, MODE);
+        }
+    }
+}
+
+template <int WALK, bool NTL, bool NTS, int MODE>
+float run(const std::vector<Lay>& sets, int reps, uint32_t grid) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((mb<WALK, NTL, NTS, MODE>), dim3(grid), dim3(256), 0, 0, sets[i % sets.size()]);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((mb<WALK, NTL, NTS, MODE>), dim3(grid), dim3(256), 0, 0, sets[(i + 3) % sets.size()]);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+float run_prod(const std::vector<Lay>& sets, int reps, uint64_t sz, uint32_t ns) {
+    std::vector<MatJob> jobs(sets.size());
+    static const uint8_t coef[R * K] = {15, 8, 6, 45, 48, 28, 153, 224, 120, 11, 231, 237, 137, 59, 179, 70, 241, 182, 186, 217, 98};
+    for (size_t i = 0; i < sets.size(); ++i) {
+        MatJob& j = jobs[i];
+        std::memset(&j, 0, sizeof j);
+        j.sz = sz;
+        j.in_sstride = K * sets[i].ld;
+        j.out_sstride = R * sets[i].ld;
+        j.nstripes = ns;
+        j.k = K;
+        j.r = R;
+        for (int q = 0; q < K; ++q) j.in[q] = sets[i].in + q * sets[i].ld;
+        for (int q = 0; q < R; ++q) j.out[q] = sets[i].out + q * sets[i].ld;
+        std::memcpy(j.coef, coef, sizeof coef);
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) CK(launch_matapply(jobs[i % jobs.size()], 0));
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) CK(launch_matapply(jobs[(i + 3) % jobs.size()], 0));
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+// The same stripes stored block-major (block j of every stripe back to back:
+// one row of ns * sz bytes per block), as fec_encode_batch collapses them:
+// one launch over 10 long streams.
+float run_prod_bm(const std::vector<Lay>& sets, int reps, uint64_t sz, uint32_t ns) {
+    std::vector<MatJob> jobs(sets.size());
+    static const uint8_t coef[R * K] = {15, 8, 6, 45, 48, 28, 153, 224, 120, 11, 231, 237, 137, 59, 179, 70, 241, 182, 186, 217, 98};
+    for (size_t i = 0; i < sets.size(); ++i) {
+        MatJob& j = jobs[i];
+        std::memset(&j, 0, sizeof j);
+        j.sz = sz * ns;
+        j.nstripes = 1;
+        j.k = K;
+        j.r = R;
+        for (int q = 0; q < K; ++q) j.in[q] = sets[i].in + q * sz * ns;
+        for (int q = 0; q < R; ++q) j.out[q] = sets[i].out + q * sz * ns;
+        std::memcpy(j.coef, coef, sizeof coef);
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) CK(launch_matapply(jobs[i % jobs.size()], 0));
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) CK(launch_matapply(jobs[(i + 3) % jobs.size()], 0));
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const uint32_t ns = argc > 2 ? atoi(argv[2]) : 256;
+    const uint64_t sz = (1u << 20) / 3 + 1;  // 349,526
+    const uint64_t ld = (sz + 255) / 256 * 256;
+    const int nsets = argc > 1 ? atoi(argv[1]) : 2;
+    const int reps = 20;
+    std::vector<Lay> sets(nsets);
+    for (auto& L : sets) {
+        CK(hipMalloc(&L.in, ns * K * ld));
+        CK(hipMalloc(&L.out, ns * R * ld));
+        CK(hipMemset(L.in, 0x5A, ns * K * ld));
+        CK(hipMemset(L.out, 0, ns * R * ld));
+        L.ld = ld;
+        L.cps = static_cast<uint32_t>(ld / 16);
+        L.units = L.cps * ns;
+    }
+    CK(hipDeviceSynchronize());
+    int ncu = 256;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    const uint32_t units = sets[0].units;
+    const uint32_t g_lane = (units + 255) / 256, g_persist = ncu * 8, g_wave4 = (units + 1023) / 1024;
+    const double enc_bytes = double(K + R) * ld * ns;
+    auto rep = [&](const char* name, float ms, double bytes) {
+        printf("%-10s %8.1f us  %7.1f GB/s  (%.3f of 8 TB/s)  sets=%d\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+               bytes / (ms * 1e-3) / 8e12, nsets);
+    };
+    for (int round = 0; round < 3; ++round) {
+        printf("-- round %d\n", round);
+        setenv("ZFEC_HIP_XCD", "1", 1);
+        rep("prod_xcd", run_prod(sets, reps, sz, ns), double(K + R) * sz * ns);
+        setenv("ZFEC_HIP_XCD", "0", 1);
+        rep("prod", run_prod(sets, reps, sz, ns), double(K + R) * sz * ns);
+        rep("prod_bm", run_prod_bm(sets, reps, sz, ns), double(K + R) * sz * ns);
+        for (int gm : {1, 2, 4, 16}) {  // grid cap = CUs x resident workgroups x gm (grid-stride beyond)
+            char nm[32];
+            snprintf(nm, sizeof nm, "prod_gm%d", gm);
+            const int keep = g_grid_mult;
+            g_grid_mult = gm;
+            rep(nm, run_prod(sets, reps, sz, ns), double(K + R) * sz * ns);
+            g_grid_mult = keep;
+        }
+        rep("lane", run<0, false, true, 0>(sets, reps, g_lane), enc_bytes);
+        rep("persist", run<1, false, true, 0>(sets, reps, g_persist), enc_bytes);
+        rep("xcd", run<2, false, true, 0>(sets, reps, g_lane), enc_bytes);
+        rep("wave4", run<3, false, true, 0>(sets, reps, g_wave4), enc_bytes);
+        rep("plain", run<0, false, false, 0>(sets, reps, g_lane), enc_bytes);
+        rep("ntload", run<0, true, true, 0>(sets, reps, g_lane), enc_bytes);
+        rep("read3", run<0, false, true, 1>(sets, reps, g_lane), double(K) * ld * ns);
+        rep("write7", run<0, false, true, 2>(sets, reps, g_lane), double(R) * ld * ns);
+        rep("copy1", run<0, false, true, 3>(sets, reps, g_lane), 2.0 * ld * ns);
+        rep("copy1_pl", run<0, false, false, 3>(sets, reps, g_lane), 2.0 * ld * ns);
+    }
+    return 0;
+}

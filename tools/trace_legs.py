@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Split a rocprofv3 kernel trace of a bench.py run into bench.py's legs.
+
+bench.py --legs-out LEGS.json records, in launch order, which leg every
+library launch belongs to ("timed loop", "encode cold", "decode warm",
+"decode fresh", ...) and the kernel it ran.  The zfec dispatches of the trace
+(kernel names in namespace zfec_hip, or zfec_hip_bitslice_*), in start-time
+order, are the same launches in the same order; this script pairs them up
+(checking every kernel name) and reports per-leg mean / min / max durations,
+the figures bench.py's roofline.launch_ms (back-to-back average) is checked
+against.
+
+    python tools/trace_legs.py LEGS.json KERNEL_TRACE.csv [OUT.json]
+    python tools/trace_legs.py LEGS.json COUNTER_COLLECTION.csv [OUT.json]
+
+With a --pmc counter_collection.csv (one row per dispatch and counter) it
+reports per-leg mean counter values instead of durations.
+"""
+import csv
+import json
+import sys
+
+
+def short(name):
+    """'void zfec_hip::(anonymous namespace)::matapply_reg<3, 7, true, ...>(zfec_hip::MatJob)' ->
+    ('matapply_reg', [3, 7]); 'zfec_hip_bitslice_k20_r40_<hash>' -> (itself, [])."""
+    n = name.replace("void zfec_hip::(anonymous namespace)::", "").split("(")[0]
+    if "<" not in n:
+        return n, []
+    base, args = n.split("<", 1)
+    return base, [a.strip() for a in args.rstrip(">").split(",")]
+
+
+def same(traced, recorded):
+    tb, ta = short(traced)
+    rb, ra = short(recorded)
+    if tb != rb:
+        return False
+    nums = [a for a in ta if a.lstrip("-").isdigit()]
+    rnums = [a for a in ra if a.lstrip("-").isdigit()]
+    return nums[:len(rnums)] == rnums
+
+
+def dispatches(path):
+    """[(order key, kernel name, {duration_us | counter: value})] of the zfec dispatches."""
+    with open(path) as f:
+        rd = list(csv.DictReader(f))
+    if rd and "Counter_Name" in rd[0]:
+        by = {}
+        for r in rd:
+            if "zfec_hip" not in r["Kernel_Name"]:
+                continue
+            d = by.setdefault(int(r["Dispatch_Id"]), (r["Kernel_Name"], {}))
+            d[1][r["Counter_Name"]] = d[1].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        return [(key, n, v) for key, (n, v) in sorted(by.items())]
+    rows = []
+    for r in rd:
+        n = r["Kernel_Name"]
+        if "zfec_hip" in n:
+            t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            rows.append((t0, n, {"duration_us": (t1 - t0) / 1e3}))
+    rows.sort(key=lambda x: x[0])
+    return rows
+
+
+def main():
+    legs = json.load(open(sys.argv[1]))
+    rows = dispatches(sys.argv[2])
+    out, i, mismatch = {}, 0, 0
+    for leg, kern, cnt in legs["legs"]:
+        vals = []
+        for _ in range(cnt):
+            if i >= len(rows):
+                break
+            _, n, v = rows[i]
+            if not same(n, kern):
+                mismatch += 1
+            vals.append(v)
+            i += 1
+        if not vals:
+            continue
+        key = "%s | %s" % (leg, kern)
+        out.setdefault(key, []).extend(vals)
+    res = {"workload": legs.get("workload"), "source": sys.argv[2].split("/")[-1], "dispatches": len(rows),
+           "paired": i, "name_mismatches": mismatch, "legs": {}}
+    for key, vals in out.items():
+        e = {"launches": len(vals)}
+        for c in sorted(vals[0]):
+            xs = [v[c] for v in vals if c in v]
+            if c == "duration_us":
+                e.update({"mean_us": round(sum(xs) / len(xs), 2), "min_us": round(min(xs), 2),
+                          "max_us": round(max(xs), 2)})
+            else:
+                e[c] = round(sum(xs) / len(xs), 1)
+        res["legs"][key] = e
+    txt = json.dumps(res, indent=1)
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as f:
+            f.write(txt + "\n")
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()

@@ -189,10 +189,21 @@ __device__ inline void store_tail(uint8_t* p, u32x4 v, uint32_t nb) {
 
 // Walks this lane's (stripe, chunk) units in grid-stride order without a
 // division per step.
+// XCD-contiguous workgroup order: workgroups are dealt round-robin over the
+// 8 XCDs (blockIdx % 8 share one); renumbering them so that each XCD's share
+// is one contiguous range of the walk lets each XCD stream its own eighth of
+// every block (a bijection on [0, gridDim.x); MI355X_MICROARCH.md, workgroup
+// dispatch).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nwg) {
+    const uint32_t q = nwg / 8, rr = nwg % 8, x = b % 8;
+    return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + b / 8;
+}
+
 struct UnitIter {
     uint32_t s, c;
     __device__ explicit UnitIter(const MatJob& job) {
-        const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+        const uint32_t wg = job.xcd_swizzle ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+        const uint32_t gid = wg * kBlock + threadIdx.x;
         s = gid / job.cps;
         c = gid - s * job.cps;
     }
@@ -1172,6 +1183,11 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
             for (int q = 0; q < 5; ++q) job.tab[i * 5 + q] = kHostBank.w[c[i] * 8 + q];
         job.tables = 1;
     }
+    // XCD-contiguous order: off by default (ZFEC_HIP_XCD=1 for A/B runs;
+    // measured 2 % slower on 256 x 1 MiB K=3/M=10 encodes from cold caches,
+    // tools/mb_cold.hip, profiles/r02_mb_cold.log)
+    const char* xe = getenv("ZFEC_HIP_XCD");
+    job.xcd_swizzle = (xe && xe[0] == '1') && !v->rows;
     hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, job);
     t_last_kernel = v->name;
     return hipGetLastError();

@@ -33,6 +33,8 @@ struct alignas(16) MatJob {
     uint32_t accumulate;   // 1: out ^= result (continuation pass for k > kMaxIn)
     uint32_t tables;       // set by launch_matapply: 1 = tab[] holds the per-coefficient tables,
                            // 2 = coef[] is in matapply_bsg's walk order
+    uint32_t xcd_swizzle;  // set by launch_matapply: 1 = workgroups dealt XCD-contiguously (UnitIter)
+    uint32_t pad_;
     const uint8_t* in[kMaxIn];
     uint8_t* out[kMaxOut];
     union {
