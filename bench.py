@@ -147,15 +147,22 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-def pmc_traffic(workload):
-    """Per-launch HBM bytes of the encode kernel from the committed PMC summary
-    (profiles/pmc_summary.json, made by tools/profile_round.sh + tools/pmc_summary.py)."""
+PROFILE_ROUND = "r02"
+
+
+def pmc_traffic(workload, leg="encode cold"):
+    """HBM bytes per launch of one bench leg from the committed per-leg PMC
+    summary (profiles/<round>_legs_<workload>.json: tools/profile_r02.sh +
+    tools/legs_summary.py; (2 * FETCH_SIZE + WRITE_SIZE) KiB per launch)."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
-            d = json.load(f)
-        return d.get("encode_" + workload, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+        with open(os.path.join(ROOT, "profiles", "%s_legs_%s.json" % (PROFILE_ROUND, workload))) as f:
+            legs = json.load(f)["legs"]
+        for key, v in legs.items():
+            if key.startswith(leg + " |"):
+                return v.get("traffic_bytes")
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 # VALU issue ceiling: 256 CUs x 4 SIMDs x ~2.4 GHz / 4.25 cycles per VOP3 wave-instruction
@@ -686,6 +693,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(gbps(enc_bytes, t["enc_ms"]), 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(gbps(enc_bytes, t["enc_ms"]) / HBM_PEAK_GBPS, 4),
                      "traffic": None if args.slabs else pmc_traffic(args.workload),
+                     "traffic_warm": None if args.slabs else pmc_traffic(args.workload, "encode warm"),
                      "kernel": "%s (encode)" % t["kernels"]["encode"], "algorithmic_bytes_per_launch": enc_bytes,
                      "launch_ms": round(t["enc_ms"], 4),
                      "achieved_warm": round(gbps(enc_bytes, t["enc_ms_warm"]), 1),
