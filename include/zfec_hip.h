@@ -97,6 +97,8 @@ enum {
                                       each row ends on a whole cache line; output bytes past sz are
                                       then unspecified.  Used only when the block and stripe strides
                                       leave that much room; otherwise ignored */
+#define FEC_FLAG_NO_POPULATE 32u   /* large pageable host outputs: do not pre-fault them from several
+                                      threads before page-locking them (A/B runs; results identical) */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);

@@ -860,3 +860,25 @@ def test_tensor_batch_api(k, m, sz, ns, block_major):
         bad = [1, 0] + list(range(k, k + k - 2)) if k > 2 else [1, 0]
         with pytest.raises(zfec_amd.Error):
             zfec_amd.Decoder(k, m).decode_batch(recv, bad)  # primary off its slot
+
+
+@pytest.mark.parametrize("chunk", [None, 65536, 3 << 20])
+def test_large_pageable_bytes_path(chunk, monkeypatch):
+    """Large pageable host blocks (bytes / numpy views sharing pages) take the
+    chunked page-locking zero-copy path (fec_abi.cpp run_pageable): parity and
+    a secondary-only decode bit-exact against the oracle, at the default chunk
+    and at chunk sizes that cut blocks at odd page offsets."""
+    if chunk:
+        monkeypatch.setenv("ZFEC_HIP_PAGEABLE_CHUNK", str(chunk))
+    k, m, sz = 3, 10, (5 << 20) + 123
+    rng = np.random.default_rng(sz)
+    flat = rng.integers(0, 256, size=k * sz, dtype=np.uint8)
+    data = flat.reshape(k, sz)
+    views = [data[i] for i in range(k)]  # adjacent blocks share pages
+    out = zfec_amd.Encoder(k, m).encode(views)
+    par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+    assert (par == oracle.encode(k, m, data)).all()
+    dec = zfec_amd.Decoder(k, m).decode(out[k:2 * k], list(range(k, 2 * k)))
+    assert b"".join(dec) == flat.tobytes()
+    sub = zfec_amd.Encoder(k, m).encode([v.tobytes() for v in views], [9, 4])
+    assert sub[0] == out[9] and sub[1] == out[4]

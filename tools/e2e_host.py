@@ -50,11 +50,20 @@ def main():
 
     enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
     out = enc.encode(blocks)
-    t = timeit(lambda: enc.encode(blocks), 5)
-    res["bytes_api_encode_GBps"] = gbps(k * sz, t)
-    t = timeit(lambda: dec.decode(out[3:6], [3, 4, 5]), 5)
-    res["bytes_api_decode_GBps"] = gbps(k * sz, t)
+    # fresh output pages pre-faulted from 4 threads (default) vs faulted by the
+    # page locking itself (ZFEC_HIP_POPULATE=0), interleaved rounds, best of each
+    for rnd in range(3):
+        for tag, val in (("", "1"), ("_nopopulate", "0")):
+            os.environ["ZFEC_HIP_POPULATE"] = val
+            t = timeit(lambda: enc.encode(blocks), 5)
+            key = "bytes_api_encode_GBps" + tag
+            res[key] = max(res.get(key, 0), gbps(k * sz, t))
+            t = timeit(lambda: dec.decode(out[3:6], [3, 4, 5]), 5)
+            key = "bytes_api_decode_GBps" + tag
+            res[key] = max(res.get(key, 0), gbps(k * sz, t))
+    os.environ["ZFEC_HIP_POPULATE"] = "1"
     assert dec.decode(out[3:6], [3, 4, 5]) == blocks
+    assert enc.encode(blocks) == out
 
     # pinned host buffers through the C-ABI
     pin_in = torch.from_numpy(data.copy()).pin_memory()

@@ -234,9 +234,9 @@ class Decoder(_fec.Decoder):
                                               flags=capi.FEC_FLAG_ASYNC)
         return out
 
-    def _decode_device(self, blocks, blocknums):
-        import torch
-
+    def _check_blocknums(self, blocknums):
+        """Validated list of k block numbers (the reference's checks,
+        zfec/_fecmodule.c:429-472, plus distinctness)."""
         k, m = self.k, self.m
         try:
             nums = list(blocknums)
@@ -258,6 +258,13 @@ class Decoder(_fec.Decoder):
                 )
         if len(set(nums)) != k:
             raise Error("Precondition violation: block nums are required to be distinct")
+        return nums
+
+    def _decode_device(self, blocks, blocknums):
+        import torch
+
+        k = self.k
+        nums = self._check_blocknums(blocknums)
         bl, sz, dev = _device_blocks(blocks, k)
         objs = list(blocks)
         # primary i into slot i (zfec/_fecmodule.c:482-493)

@@ -16,6 +16,7 @@ FEC_FLAG_LIBRARY_STREAM = 2
 FEC_FLAG_ALL_PRIMARIES = 4
 FEC_FLAG_HOST_MEMORY = 8
 FEC_FLAG_ROW_PADDING = 16
+FEC_FLAG_NO_POPULATE = 32
 
 # (name, restype, argtypes) for every symbol declared in include/zfec_hip.h
 _P = ctypes.c_void_p

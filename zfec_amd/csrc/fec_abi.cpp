@@ -9,12 +9,15 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <sys/mman.h>
+#include <thread>
 #include <unistd.h>
 
 #include <unordered_map>
@@ -341,13 +344,81 @@ constexpr size_t kPipeChunk = size_t(2) << 20;
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Fault in fresh host pages before they are page-locked: a fresh output
+// `bytes` object's pages are not mapped yet, and hipHostRegister faulted them
+// in one by one (K=3/M=10, 64 MiB: 12.8 ms for 156 MB of outputs,
+// profiles/r01_host_breakdown.log).  MADV_POPULATE_WRITE over the ranges from
+// 4 threads maps them at ~45 GB/s on the MI355X host with transparent huge
+// pages (tools/fault_probe.c, profiles/r02_fault_probe.log); where the kernel
+// lacks it (EINVAL, before Linux 5.14) each page is written once instead.
+// The ranges' contents are unspecified afterwards (they are outputs).
+void populate_parallel(const std::vector<std::pair<uintptr_t, uintptr_t>>& ranges) {
+    static const uintptr_t page = [] {
+        const long v = sysconf(_SC_PAGESIZE);
+        return static_cast<uintptr_t>(v > 0 ? v : 4096);
+    }();
+    constexpr int kThreads = 4;
+    constexpr int kPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
+    size_t total = 0;
+    for (const auto& rg : ranges) total += rg.second - rg.first;
+    if (total < (size_t(8) << 20)) return;  // small: not worth the threads
+    // cut the ranges into kThreads page-aligned pieces of near-equal size
+    std::vector<std::vector<std::pair<uintptr_t, uintptr_t>>> parts(kThreads);
+    const size_t share = (total + kThreads - 1) / kThreads;
+    size_t acc = 0;
+    for (const auto& rg : ranges) {
+        uintptr_t a = (rg.first + page - 1) / page * page;
+        const uintptr_t e = rg.second / page * page;
+        while (a < e) {
+            const int t = static_cast<int>(std::min<size_t>(acc / share, kThreads - 1));
+            const size_t room = (size_t(t) + 1) * share - acc;
+            const uintptr_t b = std::min<uintptr_t>(e, (a + std::max<size_t>(room, page) + page - 1) / page * page);
+            parts[t].emplace_back(a, b);
+            acc += b - a;
+            a = b;
+        }
+    }
+    auto work = [](const std::vector<std::pair<uintptr_t, uintptr_t>>& pr) {
+        for (const auto& rg : pr) {
+            if (madvise(reinterpret_cast<void*>(rg.first), rg.second - rg.first, kPopulateWrite) == 0) continue;
+            for (uintptr_t q = rg.first; q < rg.second; q += page) *reinterpret_cast<volatile char*>(q) = 0;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < kThreads; ++t)
+        if (!parts[t].empty()) th.emplace_back(work, std::cref(parts[t]));
+    work(parts[0]);
+    for (auto& x : th) x.join();
+}
+
 // Pins pageable host ranges for the duration of one call (RAII), so the
 // pipeline can DMA them in place; ZFEC_HIP_REGISTER=0 disables it (the copies
 // then go through HIP's own staging of pageable memory).
+// ZFEC_HIP_TRACE_HOST=1: per-phase times of a large pageable call on stderr.
+struct HostTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    std::string line;
+    HostTrace() : on(getenv("ZFEC_HIP_TRACE_HOST") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        char b[64];
+        snprintf(b, sizeof b, " %s %.0f", what, std::chrono::duration<double, std::micro>(n - t).count());
+        line += b;
+        t = n;
+    }
+    ~HostTrace() {
+        if (on) fprintf(stderr, "zfec_hip host path (us):%s\n", line.c_str());
+    }
+};
+
 struct HostPins {
     std::vector<void*> pinned;
-    ~HostPins() {
+    ~HostPins() { release(); }
+    void release() {
         for (void* p : pinned) (void)hipHostUnregister(p);
+        pinned.clear();
     }
     // Page-lock every range [p, p + n) (merged where they share pages, since a
     // page can be registered once) for the duration of the call.
@@ -392,6 +463,13 @@ const uint8_t* mapped_block(const void* p, size_t n) {
     return static_cast<const uint8_t*>(da);
 }
 
+// ZFEC_HIP_POPULATE=1 turns on the parallel pre-faulting of fresh outputs
+// before they are locked (A/B runs; read per call)
+bool populate_enabled() {
+    const char* e = getenv("ZFEC_HIP_POPULATE");
+    return e && e[0] == '1';
+}
+
 bool register_pageable() {
     static const bool on = [] {
         const char* e = getenv("ZFEC_HIP_REGISTER");
@@ -399,6 +477,71 @@ bool register_pageable() {
     }();
     return on;
 }
+
+constexpr int FEC_EAGAIN_INTERNAL = -1;  // a page could not be locked: take another path
+
+size_t pageable_chunk() {
+    const char* e = getenv("ZFEC_HIP_PAGEABLE_CHUNK");  // bytes per block per chunk (A/B runs)
+    const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0;
+    return v >= (64u << 10) ? static_cast<size_t>(v) : size_t(4) << 20;
+}
+
+// Page-locks the host blocks of a call chunk by chunk: lock(off, len) locks
+// bytes [off, off + len) of every listed host block (whole pages; a page two
+// blocks share, or one locked by an earlier chunk, is locked once).  `fresh`
+// blocks (new outputs) may first be faulted in from several threads.  Every
+// lock is released by release() / the destructor.
+struct PageLocker {
+    std::vector<const void*> blocks;
+    std::vector<char> fresh;
+    bool populate = false;
+    HostPins pins;
+    std::vector<std::pair<uintptr_t, uintptr_t>> locked;
+
+    std::vector<std::pair<uintptr_t, uintptr_t>> unlocked_parts(uintptr_t a, uintptr_t e) const {
+        std::vector<std::pair<uintptr_t, uintptr_t>> parts{{a, e}};
+        for (const auto& L : locked) {
+            std::vector<std::pair<uintptr_t, uintptr_t>> next;
+            for (const auto& p : parts) {
+                if (L.second <= p.first || L.first >= p.second) {
+                    next.push_back(p);
+                    continue;
+                }
+                if (p.first < L.first) next.emplace_back(p.first, L.first);
+                if (L.second < p.second) next.emplace_back(L.second, p.second);
+            }
+            parts.swap(next);
+        }
+        return parts;
+    }
+
+    bool lock(size_t off, size_t len) {
+        static const uintptr_t page = [] {
+            const long v = sysconf(_SC_PAGESIZE);
+            return static_cast<uintptr_t>(v > 0 ? v : 4096);
+        }();
+        std::vector<std::pair<uintptr_t, uintptr_t>> todo, pop;
+        for (size_t b = 0; b < blocks.size(); ++b) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(blocks[b]) + off;
+            for (const auto& q : unlocked_parts(a / page * page, (a + len + page - 1) / page * page)) {
+                todo.push_back(q);
+                locked.push_back(q);
+                if (fresh[b] && populate) pop.push_back(q);
+            }
+        }
+        if (!pop.empty()) populate_parallel(pop);
+        for (const auto& q : todo) {
+            void* p = reinterpret_cast<void*>(q.first);
+            if (hipHostRegister(p, q.second - q.first, hipHostRegisterMapped) != hipSuccess) {
+                (void)hipGetLastError();
+                return false;
+            }
+            pins.pinned.push_back(p);
+        }
+        return true;
+    }
+    void release() { pins.release(); }
+};
 
 // Large host-memory call: the byte range is cut into chunks of kPipeChunk;
 // chunk c's inputs go H2D on d.h2d, its kernel runs on d.stream, its outputs
@@ -451,6 +594,79 @@ int run_pipeline(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const g
     }
     if ((e = hipStreamSynchronize(d.d2h)) != hipSuccess || (e = hipStreamSynchronize(d.stream)) != hipSuccess)
         return hip_fail(e, "hipStreamSynchronize");
+    return set_status(FEC_OK);
+}
+
+// Large pageable host blocks, zero-copy: the blocks are page-locked chunk by
+// chunk (kPageableChunk bytes of every block), each chunk's kernel launched as
+// soon as its pages are locked, so the GPU's work (the kernel reads and writes
+// host memory over PCIe) on chunk c overlaps the host's faulting and locking
+// of chunk c + 1.  Fresh output pages (new `bytes` objects) are faulted in from
+// several threads first (populate_parallel), which locks them much faster
+// than hipHostRegister faulting them one by one.  Every lock is released after
+// the stream has drained.  FEC_EAGAIN_INTERNAL when a range cannot be locked
+// (nothing is left locked; the caller falls back to the copy pipeline, which
+// recomputes every output).
+int run_pageable(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out, size_t sz,
+                 Marshal& m, hipStream_t st, unsigned flags) {
+    HostTrace tr;
+    PageLocker lk;
+    lk.populate = !(flags & FEC_FLAG_NO_POPULATE) && populate_enabled();
+    // a block already page-locked by the caller is used as it is
+    std::vector<char> host_in(k, 0), host_out(r, 0);
+    std::vector<const uint8_t*> base_in(m.zin);  // kernel-visible bases of device / caller-locked blocks
+    std::vector<uint8_t*> base_out(m.zout);
+    for (int i : m.in_host) {
+        const uint8_t* z = mapped_block(in[i], sz);
+        if (z) base_in[i] = z;
+        else {
+            host_in[i] = 1;
+            lk.blocks.push_back(in[i]);
+            lk.fresh.push_back(0);
+        }
+    }
+    for (int i : m.out_host) {
+        const uint8_t* z = mapped_block(out[i], sz);
+        if (z) base_out[i] = const_cast<uint8_t*>(z);
+        else {
+            host_out[i] = 1;
+            lk.blocks.push_back(out[i]);
+            lk.fresh.push_back(1);
+        }
+    }
+    auto fail = [&]() {
+        (void)hipStreamSynchronize(st);  // chunks already launched read / write locked pages
+        lk.release();
+        return FEC_EAGAIN_INTERNAL;
+    };
+    std::vector<const uint8_t*> zin(k);
+    std::vector<uint8_t*> zout(r);
+    const size_t C = pageable_chunk();
+    tr.mark("classify");
+    for (size_t off = 0; off < sz; off += C) {
+        const size_t len = std::min(C, sz - off);
+        if (!lk.lock(off, len)) return fail();
+        tr.mark("lock");
+        for (unsigned j = 0; j < k; ++j) {
+            zin[j] = base_in[j] + off;
+            if (host_in[j] && !(zin[j] = mapped_block(in[j] + off, len))) return fail();
+        }
+        for (unsigned i = 0; i < r; ++i) {
+            zout[i] = base_out[i] + off;
+            if (host_out[i] && !(zout[i] = const_cast<uint8_t*>(mapped_block(out[i] + off, len)))) return fail();
+        }
+        if (apply_matrix(coef, k, r, zin.data(), zout.data(), len, 1, 0, 0, st)) {
+            const int e = t_status;
+            (void)hipStreamSynchronize(st);
+            return e;
+        }
+        tr.mark("launch");
+    }
+    const hipError_t e = hipStreamSynchronize(st);
+    tr.mark("sync");
+    lk.release();
+    tr.mark("unregister");
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return set_status(FEC_OK);
 }
 
@@ -509,15 +725,8 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         // large pageable blocks: page-lock them for the call and go zero-copy;
         // the chunked copy pipeline is the fallback when they cannot be mapped
         if (register_pageable()) {
-            HostPins pins;
-            std::vector<std::pair<uintptr_t, uintptr_t>> ranges;
-            for (int i : m.in_host)
-                if (!mapped_block(in[i], sz)) ranges.emplace_back(reinterpret_cast<uintptr_t>(in[i]),
-                                                                  reinterpret_cast<uintptr_t>(in[i]) + sz);
-            for (int i : m.out_host)
-                if (!mapped_block(out[i], sz)) ranges.emplace_back(reinterpret_cast<uintptr_t>(out[i]),
-                                                                   reinterpret_cast<uintptr_t>(out[i]) + sz);
-            if (pins.pin_all(ranges) && map_all()) return zero_copy(false);  // unpinned on return: synchronous
+            const int st0 = run_pageable(coef, k, r, in, out, sz, m, st, flags);
+            if (st0 != FEC_EAGAIN_INTERNAL) return st0;
         }
         return run_pipeline(*d, coef, k, r, in, out, sz, m, st);
     }
