@@ -4,8 +4,13 @@ encode and secondary-only decode from Python bytes), interleaved rounds:
 
   ZFEC_HIP_PAGEABLE_CHUNK  bytes of every block per chunk of pages locked
                          at a time (32 MiB: the whole 22 MiB block at once)
-  ZFEC_HIP_POPULATE      1: fresh outputs pre-faulted from 4 threads before
-                         they are locked
+  populate               1: each chunk's fresh outputs pre-faulted from 4
+                         threads right before it is locked
+                         (ZFEC_HIP_POPULATE=1); 0 (default): the locking
+                         faults them.  (A third variant, background threads
+                         faulting the outputs chunk by chunk ahead of the
+                         locking, measured no better and was dropped:
+                         profiles/r02_host_ab.log)
 
 Prints one line per variant (median / best GB/s of input over the rounds) and
 a JSON summary.  ZFEC_HIP_TRACE_HOST=1 in the environment adds the library's
@@ -38,13 +43,14 @@ def main():
     enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
     ref = enc.encode(blocks)
     variants = []
-    for chunk in (2 << 20, 4 << 20, 8 << 20, 32 << 20):
+    for chunk in (2 << 20, 4 << 20, 8 << 20):
         for pop in ("0", "1"):
             variants.append(("zerocopy", chunk, pop))
     res = {v: {"enc": [], "dec": []} for v in variants}
     for _ in range(a.rounds):
         for v in variants:
-            os.environ["ZFEC_HIP_PAGEABLE_CHUNK"], os.environ["ZFEC_HIP_POPULATE"] = str(v[1]), v[2]
+            os.environ["ZFEC_HIP_PAGEABLE_CHUNK"] = str(v[1])
+            os.environ["ZFEC_HIP_POPULATE"] = "1" if v[2] == "1" else "0"
             t0 = time.perf_counter()
             out = enc.encode(blocks)
             t1 = time.perf_counter()
