@@ -27,11 +27,12 @@ def need_gpu():
         pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
 
 
-@pytest.fixture(params=[("2", "0"), ("4", "0"), ("2", "1")], ids=["phase2", "phase4", "phase2_sb"])
+@pytest.fixture(params=[("2", "0", "0"), ("4", "0", "0"), ("2", "1", "0"), ("2", "0", "1")],
+                ids=["phase2", "phase4", "phase2_sb", "phase2_bb"])
 def bsg_only(request):
     """JIT off, generic kernel on; the variant knobs are read per launch."""
     prev_j, prev_g = capi.jit_mode(capi.JIT_OFF), capi.generic_mode(1)
-    keys = ("ZFEC_HIP_BSG_PHASE", "ZFEC_HIP_BSG_SB")
+    keys = ("ZFEC_HIP_BSG_PHASE", "ZFEC_HIP_BSG_SB", "ZFEC_HIP_BSG_BB")
     old = {key: os.environ.get(key) for key in keys}
     os.environ.update(dict(zip(keys, request.param)))
     yield

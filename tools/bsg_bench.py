@@ -5,6 +5,7 @@ device-resident stripes (interleaved rounds, medians):
   table   matapply_lds (v_perm table lookups; JIT off, generic off)
   bsg     matapply_bsg<RT,2,nosb> (bit-sliced, coefficients as run-time data)
   bsg_sb  matapply_bsg<RT,2> (a scheduling barrier after each row; ZFEC_HIP_BSG_SB=1)
+  bsg_bb  matapply_bsg<RT,2,bb> (input build balanced over the 4 waves; ZFEC_HIP_BSG_BB=1)
   bsg_p4  matapply_bsg<RT,4> (4 inputs per LDS phase; ZFEC_HIP_BSG_PHASE=4)
   jit     zfec_hip_bitslice_* (bit-sliced, the matrix compiled in; hipRTC)
 
@@ -36,7 +37,8 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
 VARIANTS = [("table", capi.JIT_OFF, 0, {}), ("bsg", capi.JIT_OFF, 1, {}),
             ("bsg_p4", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_PHASE": "4"}),
-            ("bsg_sb", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_SB": "1"}), ("jit", capi.JIT_FORCE, 1, {})]
+            ("bsg_sb", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_SB": "1"}),
+            ("bsg_bb", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_BB": "1"}), ("jit", capi.JIT_FORCE, 1, {})]
 
 
 def place(nums, k):
@@ -51,6 +53,7 @@ def place(nums, k):
 def set_variant(jit, gen, env):
     os.environ.pop("ZFEC_HIP_BSG_PHASE", None)
     os.environ.pop("ZFEC_HIP_BSG_SB", None)
+    os.environ.pop("ZFEC_HIP_BSG_BB", None)
     os.environ.update(env)
     capi.jit_mode(jit)
     capi.generic_mode(gen)

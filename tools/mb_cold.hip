@@ -22,7 +22,7 @@
 //            units per lane; the default cap is 1024, i.e. one unit per lane)
 //   prod_bm  the production kernel on the same stripes stored block-major
 //            (one long row per block, as fec_encode_batch collapses them)
-// usage: tools/mb_cold.exe [buffer sets] [stripes]
+// usage: tools/mb_cold.exe [buffer sets] [stripes] | tools/mb_cold.exe sweep
 // Ceilings: read3 (only the 3 loads), write7 (only the 7 stores), copy1
 // (1 load, 1 store per unit).
 //
@@ -32,6 +32,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <string>
 #include <vector>
 
 using namespace zfec_hip;
@@ -186,7 +188,136 @@ float run_prod_bm(const std::vector<Lay>& sets, int reps, uint64_t sz, uint32_t 
 
 }  // namespace
 
+// Walk variants of matapply_reg<3,7> on one stripe per block (block-major),
+// cold: U units per lane per loop trip, prefetch of the next unit, and the grid
+// (one unit per lane, or capped at `cap` x the resident workgroups with a
+// grid-stride loop), launched directly (tables in the kernel arguments as
+// launch_matapply puts them).
+template <int U, bool PF>
+float run_walk(const std::vector<Lay>& sets, int reps, uint64_t sz, uint32_t ns, int cap) {
+    typedef void (*Fn)(const MatJob);
+    Fn fn = matapply_reg<K, R, true, U, 0, PF, 0, true>;
+    static const uint8_t coef[R * K] = {15, 8, 6, 45, 48, 28, 153, 224, 120, 11, 231, 237, 137, 59, 179, 70, 241, 182, 186, 217, 98};
+    int nb = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn), kBlock, 0));
+    int ncu = 256;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    std::vector<MatJob> jobs(sets.size());
+    for (size_t i = 0; i < sets.size(); ++i) {
+        MatJob& j = jobs[i];
+        std::memset(&j, 0, sizeof j);
+        j.sz = sz * ns;
+        j.nstripes = 1;
+        j.k = K;
+        j.r = R;
+        for (int q = 0; q < K; ++q) j.in[q] = sets[i].in + q * sz * ns;
+        for (int q = 0; q < R; ++q) j.out[q] = sets[i].out + q * sz * ns;
+        for (int c = 0; c < K * R; ++c)
+            for (int q = 0; q < 5; ++q) j.tab[c * 5 + q] = kHostBank.w[coef[c] * 8 + q];
+        j.tables = 1;
+        const uint64_t cps = (j.sz + kChunk - 1) / kChunk;
+        j.cps = static_cast<uint32_t>(cps);
+        const uint64_t lanes = (cps + U - 1) / U;
+        const uint64_t need = (lanes + kBlock - 1) / kBlock;
+        const uint64_t capb = cap ? uint64_t(ncu) * nb * cap : need;
+        const uint32_t grid = static_cast<uint32_t>(need < capb ? need : capb);
+        const uint64_t gstride = uint64_t(grid) * kBlock;
+        j.gs_s = static_cast<uint32_t>(gstride / cps);
+        j.gs_c = static_cast<uint32_t>(gstride % cps);
+        j.pad_ = grid;  // (unused by the kernel) the grid to launch
+    }
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL(fn, dim3(jobs[i % jobs.size()].pad_), dim3(kBlock), 0, 0, jobs[i % jobs.size()]);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) {
+        const MatJob& j = jobs[(i + 3) % jobs.size()];
+        hipLaunchKernelGGL(fn, dim3(j.pad_), dim3(kBlock), 0, 0, j);
+    }
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int walks() {
+    const uint64_t sz1 = (1u << 20) / 3 + 1;
+    for (uint32_t ns : {64u, 256u}) {
+        const uint64_t fp = uint64_t(K + R) * sz1 * ns;
+        const int nsets = std::max<int>(2, int((1536ull << 20) / fp) + 1);
+        std::vector<Lay> sets(nsets);
+        for (auto& L : sets) {
+            CK(hipMalloc(&L.in, ns * K * sz1));
+            CK(hipMalloc(&L.out, ns * R * sz1));
+            CK(hipMemset(L.in, 0x5A, ns * K * sz1));
+            L.ld = sz1;
+        }
+        CK(hipDeviceSynchronize());
+        const double bytes = double(K + R) * sz1 * ns;
+        for (int rnd = 0; rnd < 2; ++rnd) {
+            struct V {
+                const char* name;
+                float ms;
+            } vs[] = {
+                {"prod (dispatcher)", run_prod_bm(sets, 20, sz1, ns)},
+                {"U1 PF grid=units", run_walk<1, true>(sets, 20, sz1, ns, 0)},
+                {"U1 noPF grid=units", run_walk<1, false>(sets, 20, sz1, ns, 0)},
+                {"U2 grid=units/2", run_walk<2, false>(sets, 20, sz1, ns, 0)},
+                {"U4 grid=units/4", run_walk<4, false>(sets, 20, sz1, ns, 0)},
+                {"U2 cap=2", run_walk<2, false>(sets, 20, sz1, ns, 2)},
+                {"U4 cap=1", run_walk<4, false>(sets, 20, sz1, ns, 1)},
+                {"U1 PF cap=4", run_walk<1, true>(sets, 20, sz1, ns, 4)},
+            };
+            for (const V& v : vs)
+                printf("walk ns=%4u %-20s %8.1f us  %7.1f GB/s  (%.3f of 8 TB/s)\n", ns, v.name, v.ms * 1e3,
+                       bytes / (v.ms * 1e-3) / 1e9, bytes / (v.ms * 1e-3) / 8e12);
+        }
+        for (auto& L : sets) {
+            CK(hipFree(L.in));
+            CK(hipFree(L.out));
+        }
+    }
+    return 0;
+}
+
+// Size sweep of the production kernel on one long stripe per block (block-major),
+// cold: how the HBM fraction of a K=3/M=10 encode grows with the launch's size.
+int sweep() {
+    const uint64_t sz1 = (1u << 20) / 3 + 1;
+    for (uint32_t ns : {16u, 32u, 64u, 128u, 256u, 512u, 1024u}) {
+        const uint64_t fp = uint64_t(K + R) * sz1 * ns;
+        const int nsets = std::max<int>(2, int((1536ull << 20) / fp) + 1);
+        std::vector<Lay> sets(nsets);
+        for (auto& L : sets) {
+            CK(hipMalloc(&L.in, ns * K * sz1));
+            CK(hipMalloc(&L.out, ns * R * sz1));
+            CK(hipMemset(L.in, 0x5A, ns * K * sz1));
+            L.ld = sz1;
+        }
+        CK(hipDeviceSynchronize());
+        float best = 1e9f, sum = 0.f;
+        for (int rnd = 0; rnd < 3; ++rnd) {
+            const float ms = run_prod_bm(sets, 20, sz1, ns);
+            best = std::min(best, ms);
+            sum += ms;
+        }
+        const double bytes = double(K + R) * sz1 * ns;
+        printf("sweep ns=%4u  %8.1f MB/launch  %8.1f us  %7.1f GB/s  (%.3f of 8 TB/s) mean-of-3 %.1f us  sets=%d\n", ns,
+               bytes / 1e6, best * 1e3, bytes / (best * 1e-3) / 1e9, bytes / (best * 1e-3) / 8e12, sum / 3 * 1e3, nsets);
+        for (auto& L : sets) {
+            CK(hipFree(L.in));
+            CK(hipFree(L.out));
+        }
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
+    if (argc > 1 && std::string(argv[1]) == "walks") return walks();
     const uint32_t ns = argc > 2 ? atoi(argv[2]) : 256;
     const uint64_t sz = (1u << 20) / 3 + 1;  // 349,526
     const uint64_t ld = (sz + 255) / 256 * 256;

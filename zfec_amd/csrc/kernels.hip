@@ -763,6 +763,19 @@ __device__ __forceinline__ void write_combos(char* slot, uint32_t lane8, const u
     }
 }
 
+// One group's 15 nonzero combinations (BB walk: a wave builds one 32-byte
+// group of an input), dword g of each 8-byte entry.
+__device__ __forceinline__ void write_combos1(char* slot, uint32_t lane8g, const uint32_t (&q)[4], uint32_t base) {
+    uint32_t c[16];
+    c[0] = 0u;
+#pragma unroll
+    for (int m = 1; m < 16; ++m) {
+        const int top = 31 - __builtin_clz(m);
+        c[m] = c[m ^ (1 << top)] ^ q[top];
+        *reinterpret_cast<uint32_t*>(slot + (base + m) * 512u + lane8g) = c[m];
+    }
+}
+
 // Rows are interleaved over the waves: wave w owns rows w + 4*rr, rr < RT.
 // launch_bsg lays the coefficients out for this walk: wave w's bytes of phase
 // f are (js, rr) in order, js < P, rr < RT, at byte (w * nphases + f) *
@@ -776,8 +789,13 @@ __host__ __device__ constexpr uint32_t bsg_phase_bytes() {
     return (P * RT + 3) / 4 * 4;
 }
 
-template <int RT, int P, bool SB = true>
+// BB (P = 2 only): the build is balanced over all 4 waves, wave w transposing
+// and tabulating group w & 1 of the phase's input w >> 1 (two 16-byte loads, one
+// transpose, 15 + 15 combinations written as dwords); otherwise waves 0 and 1
+// each build both groups of one input while waves 2 and 3 wait.
+template <int RT, int P, bool SB = true, bool BB = false>
 __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
+    static_assert(!BB || P == 2, "the balanced build pairs 4 waves with 2 inputs");
     constexpr uint32_t PB = bsg_phase_bytes<P, RT>();
     constexpr int ND = PB / 4;           // coefficient dwords per wave and phase
     extern __shared__ char bsg_lds[];    // P slots of kBsgSlotBytes
@@ -801,20 +819,27 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
         uint64_t o = static_cast<uint64_t>(cu) * kBsgChunk;
         return o > sz - kBsgChunk ? sz - kBsgChunk : o;
     };
-    const bool builder = wave < static_cast<uint32_t>(P);
+    const bool builder = BB || wave < static_cast<uint32_t>(P);
+    const uint32_t bin = BB ? wave >> 1 : wave;        // the phase's input this wave builds
+    const uint32_t bgrp = BB ? (wave & 1u) : 0u;      // BB: its 32-byte group
     // the input this wave transposes next, loaded one phase ahead (the next
     // unit's first phase while the current unit's last phase computes), so a
     // phase never starts waiting on HBM
     u32x4 xin[4];
     auto load_input = [&](uint32_t su, uint32_t cu, uint32_t j) {
         const uint8_t* ip = kj->in[j] + (su * job.in_sstride + unit_off(su, cu) + lane * 16u);
-        xin[0] = load16(ip);
-        xin[1] = load16(ip + 1024);
-        xin[2] = load16(ip + 2048);
-        xin[3] = load16(ip + 3072);
+        if constexpr (BB) {
+            xin[0] = load16(ip + 2048u * bgrp);
+            xin[1] = load16(ip + 2048u * bgrp + 1024);
+        } else {
+            xin[0] = load16(ip);
+            xin[1] = load16(ip + 1024);
+            xin[2] = load16(ip + 2048);
+            xin[3] = load16(ip + 3072);
+        }
     };
     uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
-    if (builder && s < job.nstripes && wave < k) load_input(s, c, wave);
+    if (builder && s < job.nstripes && bin < k) load_input(s, c, bin);
     while (s < job.nstripes) {
         uint32_t s2 = s + job.gs_s, c2 = c + job.gs_c;  // this workgroup's next unit
         if (c2 >= job.cps) {
@@ -832,24 +857,32 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
                 for (int b = 0; b < 8; ++b) acc[rr][g][b] = 0u;
         for (uint32_t f = 0; f < nph; ++f) {
             const uint32_t j0 = f * P;
-            // build: wave w < P owns input j0 + w
-            const uint32_t jb = j0 + wave;
+            // build: input j0 + bin (BB: its group bgrp) into slot bin
+            const uint32_t jb = j0 + bin;
             if (builder && jb < k) {
-                uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
-                uint32_t g1[8] = {xin[2].x, xin[2].y, xin[2].z, xin[2].w, xin[3].x, xin[3].y, xin[3].z, xin[3].w};
-                transpose8(g0);
-                transpose8(g1);
-                char* slot = bsg_lds + wave * kBsgSlotBytes;
-                const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, l1[4] = {g1[0], g1[1], g1[2], g1[3]};
-                const uint32_t h0[4] = {g0[4], g0[5], g0[6], g0[7]}, h1[4] = {g1[4], g1[5], g1[6], g1[7]};
-                write_combos(slot, lane8, l0, l1, 0u);
-                write_combos(slot, lane8, h0, h1, 16u);
+                char* slot = bsg_lds + bin * kBsgSlotBytes;
+                if constexpr (BB) {
+                    uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
+                    transpose8(g0);
+                    const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, h0[4] = {g0[4], g0[5], g0[6], g0[7]};
+                    write_combos1(slot, lane8 + 4u * bgrp, l0, 0u);
+                    write_combos1(slot, lane8 + 4u * bgrp, h0, 16u);
+                } else {
+                    uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
+                    uint32_t g1[8] = {xin[2].x, xin[2].y, xin[2].z, xin[2].w, xin[3].x, xin[3].y, xin[3].z, xin[3].w};
+                    transpose8(g0);
+                    transpose8(g1);
+                    const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, l1[4] = {g1[0], g1[1], g1[2], g1[3]};
+                    const uint32_t h0[4] = {g0[4], g0[5], g0[6], g0[7]}, h1[4] = {g1[4], g1[5], g1[6], g1[7]};
+                    write_combos(slot, lane8, l0, l1, 0u);
+                    write_combos(slot, lane8, h0, h1, 16u);
+                }
             }
             if (builder) {  // prefetch: this unit's next phase, else the next unit's first
                 if (f + 1 < nph) {
                     if (jb + P < k) load_input(s, c, jb + P);
-                } else if (s2 < job.nstripes && wave < k) {
-                    load_input(s2, c2, wave);
+                } else if (s2 < job.nstripes && bin < k) {
+                    load_input(s2, c2, bin);
                 }
             }
             // this phase's coefficients (scalar loads, waited for before the barrier)
@@ -1032,24 +1065,27 @@ struct BsgVariant {
     int blocks_per_cu = 0;
     int phase = 4;
 };
-BsgVariant g_bsg_var[3][kBsgNumRT];  // [0: P = 4, 1: P = 2, 2: P = 2 without the per-row sched_barrier][RT index]
+// [0: P = 4, 1: P = 2, 2: P = 2 without the per-row sched_barrier, 3: as 2 with the balanced build][RT index]
+BsgVariant g_bsg_var[4][kBsgNumRT];
 std::once_flag g_bsg_once;
 std::atomic<int> g_generic{-1};
 
-template <int I, int P, bool SB>
+template <int I, int P, bool SB, bool BB = false>
 void fill_bsg() {
     constexpr int RT = kBsgRT[I];
-    BsgVariant& v = g_bsg_var[P == 4 ? 0 : (SB ? 1 : 2)][I];
-    v.fn = matapply_bsg<RT, P, SB>;
+    BsgVariant& v = g_bsg_var[P == 4 ? 0 : BB ? 3 : (SB ? 1 : 2)][I];
+    v.fn = matapply_bsg<RT, P, SB, BB>;
     v.phase = P;
-    snprintf(v.name, sizeof v.name, SB ? "matapply_bsg<%d,%d>" : "matapply_bsg<%d,%d,nosb>", RT, P);
-    if constexpr (I + 1 < kBsgNumRT) fill_bsg<I + 1, P, SB>();
+    snprintf(v.name, sizeof v.name, BB ? "matapply_bsg<%d,%d,bb>" : SB ? "matapply_bsg<%d,%d>" : "matapply_bsg<%d,%d,nosb>",
+             RT, P);
+    if constexpr (I + 1 < kBsgNumRT) fill_bsg<I + 1, P, SB, BB>();
 }
 
 void init_bsg() {
     fill_bsg<0, 4, true>();
     fill_bsg<0, 2, true>();
     fill_bsg<0, 2, false>();
+    fill_bsg<0, 2, false, true>();
 }
 
 bool bsg_eligible(const MatJob& job) {
@@ -1069,9 +1105,12 @@ hipError_t launch_bsg(MatJob& job, hipStream_t stream) {
     // (ZFEC_HIP_BSG_SB=1, A/B: a scheduling barrier after each row; without
     // it the compiler overlaps rows and uses fewer registers: cfg4 decode
     // 1679 -> 1842 GB/s of input, profiles/r02_bsg_ab.log)
+    // (ZFEC_HIP_BSG_BB=1, A/B: the input build balanced over all 4 waves)
     const char* ph = getenv("ZFEC_HIP_BSG_PHASE");
     const char* sb = getenv("ZFEC_HIP_BSG_SB");
-    BsgVariant& v = g_bsg_var[(ph && ph[0] == '4') ? 0 : (sb && sb[0] == '1') ? 1 : 2][ri];
+    const char* bb = getenv("ZFEC_HIP_BSG_BB");
+    BsgVariant& v =
+        g_bsg_var[(ph && ph[0] == '4') ? 0 : (sb && sb[0] == '1') ? 1 : (bb && bb[0] == '1') ? 3 : 2][ri];
     // coefficients in the kernel's walk order: wave w's bytes of phase f at
     // (w * nph + f) * PB, (js, rr) in order: row w + 4 * rr of input P * f + js
     const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = static_cast<uint32_t>(v.phase);
