@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <new>
 #include <string>
@@ -497,23 +498,36 @@ struct PageLocker {
     std::vector<char> fresh;
     bool populate = false;
     HostPins pins;
-    std::vector<std::pair<uintptr_t, uintptr_t>> locked;
+    std::map<uintptr_t, uintptr_t> locked;  // disjoint locked page ranges, start -> end (adjacent ones merged)
 
+    // the parts of [a, e) not locked yet
     std::vector<std::pair<uintptr_t, uintptr_t>> unlocked_parts(uintptr_t a, uintptr_t e) const {
-        std::vector<std::pair<uintptr_t, uintptr_t>> parts{{a, e}};
-        for (const auto& L : locked) {
-            std::vector<std::pair<uintptr_t, uintptr_t>> next;
-            for (const auto& p : parts) {
-                if (L.second <= p.first || L.first >= p.second) {
-                    next.push_back(p);
-                    continue;
-                }
-                if (p.first < L.first) next.emplace_back(p.first, L.first);
-                if (L.second < p.second) next.emplace_back(L.second, p.second);
-            }
-            parts.swap(next);
+        std::vector<std::pair<uintptr_t, uintptr_t>> parts;
+        auto it = locked.upper_bound(a);
+        if (it != locked.begin() && std::prev(it)->second > a) --it;
+        uintptr_t x = a;
+        for (; it != locked.end() && it->first < e && x < e; ++it) {
+            if (it->first > x) parts.emplace_back(x, it->first);
+            x = std::max(x, it->second);
         }
+        if (x < e) parts.emplace_back(x, e);
         return parts;
+    }
+
+    void mark(uintptr_t a, uintptr_t e) {
+        auto it = locked.emplace(a, e).first;
+        auto nx = std::next(it);
+        if (nx != locked.end() && nx->first == e) {  // merge with the range after
+            it->second = nx->second;
+            locked.erase(nx);
+        }
+        if (it != locked.begin()) {  // and with the one before
+            auto pv = std::prev(it);
+            if (pv->second == it->first) {
+                pv->second = it->second;
+                locked.erase(it);
+            }
+        }
     }
 
     bool lock(size_t off, size_t len) {
@@ -526,7 +540,7 @@ struct PageLocker {
             const uintptr_t a = reinterpret_cast<uintptr_t>(blocks[b]) + off;
             for (const auto& q : unlocked_parts(a / page * page, (a + len + page - 1) / page * page)) {
                 todo.push_back(q);
-                locked.push_back(q);
+                mark(q.first, q.second);
                 if (fresh[b] && populate) pop.push_back(q);
             }
         }
