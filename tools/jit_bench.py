@@ -6,7 +6,8 @@ and cfg4 (K=20/M=60, 1024 x 1 MiB stripes), encode and last-k decode.
 Variants (ZFEC_HIP_JIT_* knobs): table kernels; bit-sliced JIT kernels with
 the default options, Gray-code combination order, waves-per-SIMD register
 bounds, row tiles split across the waves of a workgroup, bit-planes shared
-through LDS (ZFEC_HIP_JIT_SHARE) at several tile heights.  Earlier rounds of
+through LDS (ZFEC_HIP_JIT_SHARE) at several tile heights, 64-bit shifts in
+the bit transposes (ZFEC_HIP_JIT_SHIFT64).  Earlier rounds of
 this A/B: profiles/r01_jit_ab.log (tile heights, store cache policies),
 profiles/r01_jit_ab2.log (split).
 
@@ -32,14 +33,12 @@ from zfec_amd import capi  # noqa: E402
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
 VARIANTS = [
     ("table", capi.JIT_OFF, {}),
-    ("share", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1"}),
-    ("share_pf1", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "1"}),
-    ("share_pf1_w4", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "1", "ZFEC_HIP_JIT_WAVES": "4"}),
-    ("share_pf0_w4", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_PREFETCH": "0", "ZFEC_HIP_JIT_WAVES": "4"}),
+    ("share", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_SHIFT64": "0"}),
+    ("shift64", capi.JIT_FORCE, {"ZFEC_HIP_JIT_SHARE": "1", "ZFEC_HIP_JIT_SHIFT64": "1"}),
 ]
 KNOBS = ("ZFEC_HIP_JIT_TILE", "ZFEC_HIP_JIT_PREFETCH", "ZFEC_HIP_JIT_BARRIER", "ZFEC_HIP_JIT_STORE",
          "ZFEC_HIP_JIT_ORDER", "ZFEC_HIP_JIT_WAVES", "ZFEC_HIP_JIT_SPLIT", "ZFEC_HIP_JIT_SHARE",
-         "ZFEC_HIP_JIT_ARGLOAD")
+         "ZFEC_HIP_JIT_ARGLOAD", "ZFEC_HIP_JIT_SHIFT64")
 
 
 def place(nums, k):
@@ -56,6 +55,7 @@ def set_variant(mode, env):
         os.environ.pop(key, None)
     os.environ.update(env)
     capi.jit_mode(mode)
+    capi.generic_mode(0)  # "table" = the table kernels, not matapply_bsg
 
 
 def main():

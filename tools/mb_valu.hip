@@ -31,6 +31,10 @@ __global__ __launch_bounds__(256) void valu_loop(uint32_t* out, uint32_t s0, uin
                 asm volatile("v_and_b32 %0, %1, %0" : "+v"(v[i]) : "v"(t));
             else if constexpr (OP == 5)  // v_xor (VOP2)
                 asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(t));
+            else if constexpr (OP == 6)  // v_lshlrev_b32 (VOP2 shift)
+                asm volatile("v_lshlrev_b32 %0, 4, %0" : "+v"(v[i]));
+            else if constexpr (OP == 7)  // v_lshl_or_b32 (VOP3)
+                asm volatile("v_lshl_or_b32 %0, %0, 4, %1" : "+v"(v[i]) : "v"(t));
         }
     }
     uint32_t acc = 0;
@@ -38,16 +42,32 @@ __global__ __launch_bounds__(256) void valu_loop(uint32_t* out, uint32_t s0, uin
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// 64-bit shifts of register pairs (8 independent chains of 64 bits): one
+// v_lshlrev_b64 moves two 32-bit words; counted here as 2 lane-ops (the two
+// dwords it shifts), so equal to v_lshlrev_b32's figure means full rate.
+__global__ __launch_bounds__(256) void valu_loop64(uint32_t* out) {
+    uint64_t v[8];
+    for (int i = 0; i < 8; ++i) v[i] = (uint64_t(threadIdx.x) << 32) * 0x01010101ull + i;
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("v_lshlrev_b64 %0, 4, %0" : "+v"(v[i]));
+    }
+    uint64_t acc = 0;
+    for (int i = 0; i < 8; ++i) acc ^= v[i];
+    if (acc == 0x12345678ull) out[0] = uint32_t(acc);
+}
+
 int main() {
     uint32_t* out;
     CK(hipMalloc(&out, 4));
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
-    const char* names[] = {"v_perm s,v,v", "v_perm s,s,v", "v_perm v,v,v", "v_bitop3 xor3", "v_and_b32", "v_xor_b32"};
+    const char* names[] = {"v_perm s,v,v", "v_perm s,s,v", "v_perm v,v,v", "v_bitop3 xor3", "v_and_b32",
+                           "v_xor_b32",   "v_lshlrev_b32", "v_lshl_or_b32", "v_lshlrev_b64 (x2)"};
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int op = 0; op < 6; ++op) {
+    for (int op = 0; op < 9; ++op) {
         for (int wps : {1, 2, 4, 8}) {  // waves per SIMD
             const int grid = p.multiProcessorCount * wps;  // 256-thread blocks = 4 waves = 1 per SIMD
             auto launch = [&] {
@@ -58,6 +78,9 @@ int main() {
                     case 3: hipLaunchKernelGGL(valu_loop<3>, grid, 256, 0, 0, out, 1u, 2u); break;
                     case 4: hipLaunchKernelGGL(valu_loop<4>, grid, 256, 0, 0, out, 1u, 2u); break;
                     case 5: hipLaunchKernelGGL(valu_loop<5>, grid, 256, 0, 0, out, 1u, 2u); break;
+                    case 6: hipLaunchKernelGGL(valu_loop<6>, grid, 256, 0, 0, out, 1u, 2u); break;
+                    case 7: hipLaunchKernelGGL(valu_loop<7>, grid, 256, 0, 0, out, 1u, 2u); break;
+                    case 8: hipLaunchKernelGGL(valu_loop64, grid, 256, 0, 0, out); break;
                 }
             };
             launch();
@@ -68,7 +91,7 @@ int main() {
             CK(hipEventSynchronize(b));
             float ms;
             CK(hipEventElapsedTime(&ms, a, b));
-            const double ops = 5.0 * grid * 256.0 * ITERS * 8;
+            const double ops = 5.0 * grid * 256.0 * ITERS * 8 * (op == 8 ? 2 : 1);
             printf("%-14s waves/SIMD=%d  %7.2f T lane-ops/s\n", names[op], wps, ops / (ms * 1e-3) / 1e12);
         }
     }

@@ -81,11 +81,45 @@ __device__ __forceinline__ void sw(u32& a, u32& b, int s, u32 m) {
     a = t0;
     b = t1;
 }
+// Two block swaps with the same shift at once: the shifts as 64-bit register
+// pairs (v_lshlrev_b64 / v_lshrrev_b64 shift two dwords at the issue rate of
+// one 32-bit shift, tools/mb_valu.hip).  The bits that cross the dword
+// boundary land exactly where the swap's mask discards them (the low s bits of
+// a byte on the left shift, the high s bits on the right shift).  Inline asm,
+// or the compiler splits the right shift back into v_alignbit + v_lshrrev.
+// Pairs (a0, a1) and (b0, b1) are adjacent registers in the first two stages
+// of tr8, where no moves are needed to form them.
+__device__ __forceinline__ u64 shl64(u64 x, int s) {
+    u64 r;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(s), "v"(x));
+    return r;
+}
+__device__ __forceinline__ u64 shr64(u64 x, int s) {
+    u64 r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(s), "v"(x));
+    return r;
+}
+__device__ __forceinline__ void sw2(u32& a0, u32& b0, u32& a1, u32& b1, int s, u32 m) {
+    const u64 bl = shl64((((u64)b1) << 32) | b0, s);
+    const u64 ar = shr64((((u64)a1) << 32) | a0, s);
+    const u32 t0 = sel(m, a0, (u32)bl), t1 = sel(m, (u32)ar, b0);
+    const u32 t2 = sel(m, a1, (u32)(bl >> 32)), t3 = sel(m, (u32)(ar >> 32), b1);
+    a0 = t0;
+    b0 = t1;
+    a1 = t2;
+    b1 = t3;
+}
 // 8 dwords (32 bytes) <-> 8 bit-planes; the transpose is its own inverse
 __device__ __forceinline__ void tr8(u32& v0, u32& v1, u32& v2, u32& v3, u32& v4, u32& v5, u32& v6, u32& v7) {
+#if ZFEC_SHIFT64
+    sw2(v0, v4, v1, v5, 4, 0x0F0F0F0Fu); sw2(v2, v6, v3, v7, 4, 0x0F0F0F0Fu);
+    sw2(v0, v2, v1, v3, 2, 0x33333333u); sw2(v4, v6, v5, v7, 2, 0x33333333u);
+    sw(v0, v1, 1, 0x55555555u); sw(v2, v3, 1, 0x55555555u); sw(v4, v5, 1, 0x55555555u); sw(v6, v7, 1, 0x55555555u);
+#else
     sw(v0, v4, 4, 0x0F0F0F0Fu); sw(v1, v5, 4, 0x0F0F0F0Fu); sw(v2, v6, 4, 0x0F0F0F0Fu); sw(v3, v7, 4, 0x0F0F0F0Fu);
     sw(v0, v2, 2, 0x33333333u); sw(v1, v3, 2, 0x33333333u); sw(v4, v6, 2, 0x33333333u); sw(v5, v7, 2, 0x33333333u);
     sw(v0, v1, 1, 0x55555555u); sw(v2, v3, 1, 0x55555555u); sw(v4, v5, 1, 0x55555555u); sw(v6, v7, 1, 0x55555555u);
+#endif
 }
 // Buffer loads / stores off a wave-uniform base (block pointer + the unit's
 // offset, in SGPRs) with the lane's 32-bit offset: no 64-bit VGPR address per
@@ -149,7 +183,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
 
     Src e;
     e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
-    e("constexpr int kStoreAux = %u;\n", opt.store_aux);
+    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", opt.store_aux, opt.shift64 ? 1 : 0);
     e.s += kPrelude;
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
     // split: the row tiles of a unit go to the waves of one workgroup, which
@@ -556,6 +590,7 @@ BsOptions options_from_env() {
     o.split = env_uint("ZFEC_HIP_JIT_SPLIT", o.split ? 1 : 0) != 0;
     o.share = env_uint("ZFEC_HIP_JIT_SHARE", o.share ? 1 : 0) != 0;
     o.argload = env_uint("ZFEC_HIP_JIT_ARGLOAD", o.argload ? 1 : 0) != 0;
+    o.shift64 = env_uint("ZFEC_HIP_JIT_SHIFT64", o.shift64 ? 1 : 0) != 0;
     if (o.waves > 8) o.waves = 8;
     return o;
 }
@@ -570,6 +605,7 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
              opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
     key += hdr;
     if (opt.argload) key += "argload/";
+    if (opt.shift64) key += "shift64/";
     if (opt.share && bitslice_split(r, opt)) key += "share/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;

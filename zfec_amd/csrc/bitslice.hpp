@@ -38,6 +38,8 @@ struct BsOptions {
     bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
     bool share = true;               // split: inputs transposed once per unit, bit-planes shared through LDS
     bool argload = true;             // block pointers loaded where used (no up-front SGPR spill)
+    bool shift64 = true;             // bit transposes shift register pairs with 64-bit shifts (4-9 % fewer
+                                     // VALU; cfg4 decode 380 -> 375 us, encode unchanged: profiles/r02_jit_shift64.log)
 };
 
 // Row tiles of an r-row matrix, and whether they go to the waves of one
