@@ -82,6 +82,11 @@ def parse():
                         "0 otherwise)")
     p.add_argument("--legs-out", default=None,
                    help="write the run's launch sequence per leg (JSON) for tools/trace_legs.py")
+    p.add_argument("--streams", type=int, default=None, choices=[1, 2],
+                   help="2: each step's encode on one stream and its decode (independent buffers) on a second "
+                        "stream, joined once after the timed steps, so short launches overlap each other's "
+                        "ramp-up and drain (default: 2 for the K=3/M=10 workloads cfg2/cfg5, 1 for the bit-sliced "
+                        "wide codes cfg3/cfg4, where co-resident launches measured slower; DESIGN.md section 5)")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -236,41 +241,26 @@ def cpu_baseline(seconds, k, m, sz):
     stripe of k*sz bytes per step, decoding from the last k blocks), one
     stripe per thread on every CPU this process may use (no cap), plus a
     1-thread figure.  Stripes are shrunk so all threads' buffers stay within
-    ~8 GB of host memory."""
+    ~8 GB of host memory.
+
+    The reference's fec.c (oracle/_ref, built from /root/reference by
+    oracle/Makefile) runs from C threads (oracle/ref_bench.c), so neither the
+    Python binding's per-call cost nor the GIL caps the CPU figure; the same
+    step through the reference's Python binding (zfec/_fecmodule.c, one Python
+    thread per CPU) is reported beside it.  Without oracle/_ref the oracle
+    restatement runs instead (kind "port")."""
     from oracle import oracle
 
-    ref = oracle.ref_module()
     cpus = host_cpus()
     threads = cpus["usable"]
     sz = max(1, min(sz, (8 << 30) // (threads * (m + k))))
+    nums = place(list(range(m - k, m)), k)  # the same last-k decode set as the GPU leg
+    rb = oracle.ref_bench_lib()
+    mod = oracle.ref_module()
     rng = np.random.default_rng(7)
     proto = [rng.integers(0, 256, size=sz, dtype=np.uint8).tobytes() for _ in range(k)]
-    nums = place(list(range(m - k, m)), k)  # the same last-k decode set as the GPU leg
-    if ref is not None:
-        kind = "reference"
 
-        def make_work(counts, stop):
-            def work(t):
-                enc, dec = ref.Encoder(k, m), ref.Decoder(k, m)
-                blocks = [bytes(b) for b in proto]
-                while not stop.is_set():
-                    out = enc.encode(blocks)
-                    dec.decode([out[n] for n in nums], nums)
-                    counts[t] += 1
-            return work
-    else:
-        kind = "port"
-        data = np.frombuffer(b"".join(proto), dtype=np.uint8).reshape(k, sz)
-
-        def make_work(counts, stop):
-            def work(t):
-                while not stop.is_set():
-                    allb = np.concatenate([data, oracle.encode(k, m, data)])
-                    oracle.decode(k, m, allb[nums], nums)
-                    counts[t] += 1
-            return work
-
-    def run(nthreads, secs):
+    def py_run(make_work, nthreads, secs):
         counts = [0] * nthreads
         stop = threading.Event()
         work = make_work(counts, stop)
@@ -282,21 +272,58 @@ def cpu_baseline(seconds, k, m, sz):
         stop.set()
         for th in ths:
             th.join()
-        el = time.perf_counter() - t0  # threads finish their step in flight; all of it is counted
-        return sum(counts), el
+        return sum(counts), time.perf_counter() - t0  # steps in flight at the stop are counted
 
-    steps1, el1 = run(1, max(2.0, seconds * 0.3))
-    steps, el = run(threads, seconds)
-    src = ("reference zfec/fec.c+_fecmodule.c compiled by oracle/Makefile (-O2 -march=x86-64-v2)"
-           if kind == "reference" else "oracle/fec_oracle.c restatement")
-    return {"value": round(steps * 2 * k * sz / el / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": kind,
-            "value_1thread": round(steps1 * 2 * k * sz / el1 / 1e9, 4),
-            "host": cpus,
-            "sample": "%d steps (encode + last-k decode of a K=%d/M=%d %d-byte stripe) in %.1f s on %d threads, "
-                      "one stripe per thread, every CPU the process may use (affinity %d, cgroup quota %s, "
-                      "os.cpu_count %s); 1 thread: %d steps in %.1f s; %s" % (
-                          steps, k, m, k * sz, el, threads, cpus["affinity"], cpus["cgroup_quota_cpus"],
-                          cpus["os_cpu_count"], steps1, el1, src)}
+    def binding_work(counts, stop):
+        def work(t):
+            enc, dec = mod.Encoder(k, m), mod.Decoder(k, m)
+            blocks = [bytes(b) for b in proto]
+            while not stop.is_set():
+                out = enc.encode(blocks)
+                dec.decode([out[n] for n in nums], nums)
+                counts[t] += 1
+        return work
+
+    def port_work(counts, stop):
+        data = np.frombuffer(b"".join(proto), dtype=np.uint8).reshape(k, sz)
+
+        def work(t):
+            while not stop.is_set():
+                allb = np.concatenate([data, oracle.encode(k, m, data)])
+                oracle.decode(k, m, allb[nums], nums)
+                counts[t] += 1
+        return work
+
+    rate = lambda steps, el: round(steps * 2 * k * sz / el / 1e9, 4)
+    extra = {}
+    if rb is not None:
+        kind, how = "reference", ("reference zfec/fec.c compiled by oracle/Makefile (-O2 -march=x86-64-v2), "
+                                  "driven from C threads (oracle/ref_bench.c)")
+        steps, el = oracle.ref_bench(rb, k, m, sz, threads, seconds)
+        steps1, el1 = oracle.ref_bench(rb, k, m, sz, 1, max(2.0, seconds * 0.3))
+        if mod is not None:
+            sb, eb = py_run(binding_work, threads, max(2.0, seconds * 0.3))
+            extra["value_python_binding"] = rate(sb, eb)
+            extra["python_binding"] = ("the same step through the reference's own Python binding (_fecmodule.c) "
+                                       "from %d Python threads: %d steps in %.1f s" % (threads, sb, eb))
+    elif mod is not None:
+        kind, how = "reference", "reference zfec/_fecmodule.c + fec.c (oracle/Makefile), one Python thread per CPU"
+        steps, el = py_run(binding_work, threads, seconds)
+        steps1, el1 = py_run(binding_work, 1, max(2.0, seconds * 0.3))
+    else:
+        kind, how = "port", "oracle/fec_oracle.c restatement, one Python thread per CPU"
+        steps, el = py_run(port_work, threads, seconds)
+        steps1, el1 = py_run(port_work, 1, max(2.0, seconds * 0.3))
+    out = {"value": rate(steps, el), "unit": "GB/s", "cores": threads, "kind": kind,
+           "value_1thread": rate(steps1, el1),
+           "host": cpus,
+           "sample": "%d steps (encode + last-k decode of a K=%d/M=%d %d-byte stripe) in %.1f s on %d threads, "
+                     "one stripe per thread, every CPU the process may use (affinity %d, cgroup quota %s, "
+                     "os.cpu_count %s); 1 thread: %d steps in %.1f s; %s" % (
+                         steps, k, m, k * sz, el, threads, cpus["affinity"], cpus["cgroup_quota_cpus"],
+                         cpus["os_cpu_count"], steps1, el1, how)}
+    out.update(extra)
+    return out
 
 
 def bench_zfec_style(Encoder, Decoder, k=3, m=10, size=10 ** 6, reps=1000):
@@ -376,7 +403,8 @@ def back_to_back(fns, n, stream, leg):
     return a.elapsed_time(b) / n, host_us
 
 
-def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True, fresh=0):
+def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True, fresh=0,
+                 streams=1):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
@@ -448,7 +476,29 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
         enc(stream.cuda_stream)
         dec(stream.cuda_stream)
 
-    if use_graph:
+    fork = join = lambda: None
+    if streams == 2:
+        # a step's encode and decode touch disjoint buffers: encodes in order on
+        # one stream, decodes on another, so each launch's ramp-up and drain
+        # overlap the other stream's work; the streams fork from the launch
+        # stream before the steps and join it after them (no per-step join)
+        s_enc, s_dec = torch.cuda.Stream(), torch.cuda.Stream()
+
+        def step():
+            enc(s_enc.cuda_stream)
+            dec(s_dec.cuda_stream)
+
+        def fork():
+            s_enc.wait_stream(stream)
+            s_dec.wait_stream(stream)
+
+        def join():
+            stream.wait_stream(s_enc)
+            stream.wait_stream(s_dec)
+
+        launch = "eager, 2 streams (encodes | decodes)"
+
+    if use_graph and streams == 1:
         try:
             cap = torch.cuda.Stream()
             graph = torch.cuda.CUDAGraph()
@@ -465,24 +515,33 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
             launch = "hipGraph (1 replay per step)"
         except Exception as e:  # capture unsupported: keep eager launches
             launch = "eager (graph capture failed: %s: %s)" % (type(e).__name__, str(e)[:120])
+    fork()
     for _ in range(3):
         step()
-        if launch == "eager":
+        if launch.startswith("eager"):
             LEGS.add("warmup", kernels["encode"])
             LEGS.add("warmup", kernels["decode"])
+    join()
     torch.cuda.synchronize()
     barrier(dist)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
+    fork()
     for _ in range(steps):
         step()
+    join()
     e1.record(stream)
     torch.cuda.synchronize()
     barrier(dist)
     el = time.perf_counter() - t0
-    if launch == "eager":
+    # the timed steps' results are the code's: decode(encode(x)) == x
+    assert torch.equal(rec[0][:, :, :sz], data[0][:, missing, :sz]), "timed loop: decode(encode(x)) != x"
+    for j, s in enumerate(slots):  # and the timed encodes rewrote the parity the decodes read
+        if s >= k:
+            assert torch.equal(par[0][:, s - k, :sz], recv[0][:, j, :sz]), "timed loop: parity changed"
+    if launch.startswith("eager"):
         for _ in range(steps):
             LEGS.add("timed loop", kernels["encode"])
             LEGS.add("timed loop", kernels["decode"])
@@ -641,7 +700,10 @@ def main():
     else:
         ns = nstripes
     fresh = args.fresh if args.fresh is not None else (20 if args.workload in ("cfg3", "cfg4") else 0)
+    if args.streams is None:
+        args.streams = 1 if args.workload in ("cfg3", "cfg4") else 2
     t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout,
+                     streams=args.streams,
                      row_padding=not args.no_row_padding, fresh=fresh if rank == 0 else 0)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
@@ -711,6 +773,7 @@ def main():
                             "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4)},
         "valu_roofline": None if args.slabs else valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
+        "streams": args.streams,
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
         "encode_input_GBps": round(gbps(k * sz * ns, t["enc_ms"]), 1),
         "decode_input_GBps": round(gbps(k * sz * ns, t["dec_ms"]), 1),

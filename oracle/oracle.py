@@ -134,6 +134,32 @@ def pattern_blocks(k, sz):
     return out
 
 
+def ref_bench_lib():
+    """oracle/_ref/libref_bench.so (ref_bench.c + the reference's fec.c): the
+    reference's CPU path driven from C threads, or None if unbuilt."""
+    import ctypes
+
+    path = os.path.join(REF_DIR, "libref_bench.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.ref_bench.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
+                              ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
+    lib.ref_bench.restype = ctypes.c_int
+    return lib
+
+
+def ref_bench(lib, k, m, sz, threads, seconds):
+    """(steps, seconds) of `threads` C threads each repeating encode + last-k
+    decode of its own K/M stripe of k*sz bytes for ~`seconds` (ref_bench.c)."""
+    import ctypes
+
+    st, el = ctypes.c_uint64(), ctypes.c_double()
+    if lib.ref_bench(k, m, sz, threads, seconds, ctypes.byref(st), ctypes.byref(el)) != 0:
+        raise RuntimeError("ref_bench failed (allocation, threads, or a wrong decode)")
+    return st.value, el.value
+
+
 def ref_module():
     """The real reference extension (oracle/_ref/_fec*.so) or None if unbuilt."""
     if not os.path.isdir(REF_DIR):

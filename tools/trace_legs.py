@@ -58,7 +58,9 @@ def dispatches(path):
         n = r["Kernel_Name"]
         if "zfec_hip" in n:
             t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-            rows.append((t0, n, {"duration_us": (t1 - t0) / 1e3}))
+            # enqueue order (launches on two streams may start out of it)
+            key = int(r["Dispatch_Id"]) if r.get("Dispatch_Id") else t0
+            rows.append((key, n, {"duration_us": (t1 - t0) / 1e3}))
     rows.sort(key=lambda x: x[0])
     return rows
 
