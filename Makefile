@@ -24,13 +24,16 @@ $(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp $(SRC)/bitslice.hpp
 $(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp include/zfec_hip.h
+$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/host_pool.hpp include/zfec_hip.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(SRC)/gf256.o: $(SRC)/gf256.cpp $(SRC)/gf256.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o
+$(SRC)/host_pool.o: $(SRC)/host_pool.cpp $(SRC)/host_pool.hpp
+	$(CXX) -O2 -std=c++17 -fPIC -fvisibility=hidden -Wall -c $< -o $@
+
+$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o $(SRC)/host_pool.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -lpthread
 
 $(PYEXT): $(SRC)/fecmodule.cpp include/zfec_hip.h $(LIB)

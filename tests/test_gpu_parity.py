@@ -251,8 +251,8 @@ def _encode_ptrs_check(code, k, m, data, in_addrs, out_addrs, read_out, sz):
 
 
 def test_c_abi_large_pageable_host_blocks_sharing_pages():
-    """> 4 MiB of pageable host blocks: page-locked for the call (ranges that
-    share pages merged) and read / written by the kernel in place."""
+    """> 4 MiB of pageable host blocks sharing pages, at odd offsets with guard
+    bytes: staged through the pinned slots (default host path)."""
     k, m = 3, 10
     code = capi.Code(k, m)
     rng = np.random.default_rng(17)
@@ -862,14 +862,18 @@ def test_tensor_batch_api(k, m, sz, ns, block_major):
             zfec_amd.Decoder(k, m).decode_batch(recv, bad)  # primary off its slot
 
 
-@pytest.mark.parametrize("chunk", [None, 65536, 3 << 20])
-def test_large_pageable_bytes_path(chunk, monkeypatch):
-    """Large pageable host blocks (bytes / numpy views sharing pages) take the
-    chunked page-locking zero-copy path (fec_abi.cpp run_pageable): parity and
-    a secondary-only decode bit-exact against the oracle, at the default chunk
+@pytest.mark.parametrize("path,chunk", [("stage", None), ("stage", 65536), ("stage", 3 << 20),
+                                        ("lock", None), ("lock", 65536), ("lock", 3 << 20), ("copy", None)])
+def test_large_pageable_bytes_path(path, chunk, monkeypatch):
+    """Large pageable host blocks (bytes / numpy views sharing pages) take one
+    of the host paths (fec_abi.cpp): staged through pinned slots by the host
+    copy threads (run_staged, the default), page-locked chunk by chunk
+    (run_pageable) or the DMA pipeline (run_pipeline).  Parity and a
+    secondary-only decode bit-exact against the oracle, at the default chunk
     and at chunk sizes that cut blocks at odd page offsets."""
+    monkeypatch.setenv("ZFEC_HIP_HOST_PATH", path)
     if chunk:
-        monkeypatch.setenv("ZFEC_HIP_PAGEABLE_CHUNK", str(chunk))
+        monkeypatch.setenv("ZFEC_HIP_PAGEABLE_CHUNK" if path == "lock" else "ZFEC_HIP_STAGE_CHUNK", str(chunk))
     k, m, sz = 3, 10, (5 << 20) + 123
     rng = np.random.default_rng(sz)
     flat = rng.integers(0, 256, size=k * sz, dtype=np.uint8)

@@ -29,6 +29,7 @@
 #include "../../include/zfec_hip.h"
 #include "bitslice.hpp"
 #include "gf256.hpp"
+#include "host_pool.hpp"
 #include "kernels.hpp"
 
 #define FEC_API extern "C" __attribute__((visibility("default")))
@@ -67,6 +68,7 @@ bool valid_code(const fec_t* c) { return c && c->enc_matrix && c->magic == magic
 // ---- per-thread, per-device staging -----------------------------------------
 
 constexpr int kSlots = 3;  // pipeline depth of the host path (H2D | kernel | D2H)
+constexpr int kStageSlots = 3;  // staged host path: copy-in | kernel | copy-out
 
 struct DevCtx {
     hipStream_t stream = nullptr;  // library stream: kernels of the host path, sync calls
@@ -78,6 +80,10 @@ struct DevCtx {
     void* hbuf = nullptr;  // pinned
     void* hbuf_dev = nullptr;  // its address in the device's view (kernels read / write it over PCIe)
     size_t hcap = 0;
+    void* sbuf = nullptr;  // pinned staging slots of the staged host path
+    void* sbuf_dev = nullptr;
+    size_t scap = 0;
+    hipEvent_t ev_stg[kStageSlots] = {};
 };
 
 struct ThreadCtx {
@@ -97,8 +103,11 @@ struct ThreadCtx {
                 if (d.ev_out[i]) (void)hipEventDestroy(d.ev_out[i]);
             }
             if (d.ev_start) (void)hipEventDestroy(d.ev_start);
+            for (int i = 0; i < kStageSlots; ++i)
+                if (d.ev_stg[i]) (void)hipEventDestroy(d.ev_stg[i]);
             if (d.dbuf) (void)hipFree(d.dbuf);
             if (d.hbuf) (void)hipHostFree(d.hbuf);
+            if (d.sbuf) (void)hipHostFree(d.sbuf);
             (void)hipSetDevice(cur);
         }
     }
@@ -685,6 +694,157 @@ int run_pageable(const uint8_t* coef, unsigned k, unsigned r, const gf* const* i
     return set_status(FEC_OK);
 }
 
+// Host path for large pageable calls (ZFEC_HIP_HOST_PATH, read per call for
+// A/B runs): "stage" (run_staged), "lock" (run_pageable) or "copy"
+// (run_pipeline with HIP's own staging of pageable memory).
+enum class HostPath { kStage, kLock, kCopy };
+
+HostPath host_path() {
+    const char* e = getenv("ZFEC_HIP_HOST_PATH");
+    if (e && !strcmp(e, "lock")) return HostPath::kLock;
+    if (e && !strcmp(e, "copy")) return HostPath::kCopy;
+    return HostPath::kStage;
+}
+
+// Bytes of every host block per staged chunk: ZFEC_HIP_STAGE_CHUNK, else
+// about 16 MiB of staging per chunk over all host blocks, in whole 64 KiB
+// (K=3/M=10, 64 MiB from bytes: 8 MiB chunks 8.7 GB/s encode, 16-20 MiB 9.3;
+// 2.5 MiB 6.4; profiles/r02_host_stage_ab.log).
+size_t staged_chunk(size_t nblocks) {
+    const char* e = getenv("ZFEC_HIP_STAGE_CHUNK");
+    const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0;
+    if (v >= (64u << 10)) return static_cast<size_t>(v) / 4096 * 4096;
+    const size_t total = size_t(16) << 20;
+    return std::max<size_t>(256u << 10, total / std::max<size_t>(1, nblocks) / (64u << 10) * (64u << 10));
+}
+
+int ensure_sbuf(DevCtx& d, size_t bytes) {
+    if (!d.ev_stg[0])
+        for (int i = 0; i < kStageSlots; ++i) {
+            hipError_t e = hipEventCreateWithFlags(&d.ev_stg[i], hipEventDisableTiming);
+            if (e != hipSuccess) return hip_fail(e, "staging events");
+        }
+    if (bytes <= d.scap) return FEC_OK;
+    if (d.sbuf) {
+        (void)hipDeviceSynchronize();  // no kernel of an earlier call may still use the old slots
+        (void)hipHostFree(d.sbuf);
+        d.sbuf = d.sbuf_dev = nullptr;
+        d.scap = 0;
+    }
+    hipError_t e = hipHostMalloc(&d.sbuf, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return set_status(FEC_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    if ((e = hipHostGetDevicePointer(&d.sbuf_dev, d.sbuf, 0)) != hipSuccess || !d.sbuf_dev) {
+        (void)hipGetLastError();
+        d.sbuf_dev = d.sbuf;
+    }
+    d.scap = bytes;
+    return FEC_OK;
+}
+
+// Large pageable host blocks, staged: nothing of the caller's is page-locked.
+// The byte range is cut into chunks; for chunk c the host threads (HostPool)
+// copy the input blocks' bytes into a pinned staging slot, the kernel reads
+// that slot and writes the outputs into the slot over PCIe (zero-copy), and
+// the threads copy the outputs out into the caller's blocks -- faulting in
+// fresh output pages (new `bytes` objects, zfec/_fecmodule.c:206-242) on every
+// pool thread at once.  kStageSlots slots rotate, so copy-in of chunk c + 1 and
+// copy-out of chunk c - 1 run while chunk c's kernel does.  Replaces
+// hipHostRegister of every block (run_pageable), whose cost is the kernel
+// mapping each fresh page one by one.  Device-resident and
+// caller-locked blocks are read / written in place.
+int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out,
+               size_t sz, Marshal& m, hipStream_t st) {
+    HostTrace tr;
+    std::vector<char> host_in(k, 0), host_out(r, 0);
+    std::vector<const uint8_t*> base_in(m.zin);  // kernel-visible bases of device / caller-locked blocks
+    std::vector<uint8_t*> base_out(m.zout);
+    std::vector<unsigned> sin, sout;  // staged blocks
+    for (int i : m.in_host) {
+        const uint8_t* z = mapped_block(in[i], sz);
+        if (z) base_in[i] = z;
+        else {
+            host_in[i] = 1;
+            sin.push_back(static_cast<unsigned>(i));
+        }
+    }
+    for (int i : m.out_host) {
+        const uint8_t* z = mapped_block(out[i], sz);
+        if (z) base_out[i] = const_cast<uint8_t*>(z);
+        else {
+            host_out[i] = 1;
+            sout.push_back(static_cast<unsigned>(i));
+        }
+    }
+    const size_t nin = sin.size(), nout = sout.size();
+    const size_t C = staged_chunk(nin + nout);
+    const size_t slot_bytes = C * (nin + nout);
+    if (ensure_sbuf(d, slot_bytes * kStageSlots)) return t_status;
+    uint8_t* const hs = static_cast<uint8_t*>(d.sbuf);
+    uint8_t* const ds = static_cast<uint8_t*>(d.sbuf_dev);
+    HostPool& pool = HostPool::get();
+    CopyLatch lin[kStageSlots], lout[kStageSlots];
+    const size_t nchunks = (sz + C - 1) / C;
+    tr.mark("classify");
+
+    auto stage_in = [&](size_t c) {
+        const int s = static_cast<int>(c % kStageSlots);
+        const size_t off = c * C, len = std::min(C, sz - off);
+        for (size_t q = 0; q < nin; ++q)
+            pool.copy_async(hs + s * slot_bytes + q * C, in[sin[q]] + off, len, &lin[s], len);
+    };
+    auto copy_out = [&](size_t c) {
+        const int s = static_cast<int>(c % kStageSlots);
+        const size_t off = c * C, len = std::min(C, sz - off);
+        const size_t piece = std::max<size_t>(256u << 10, len / 4);
+        for (size_t q = 0; q < nout; ++q)
+            pool.copy_async(out[sout[q]] + off, hs + s * slot_bytes + (nin + q) * C, len, &lout[s], piece);
+    };
+    // every queued copy references the caller's buffers and the slots: all of
+    // them finish before this returns, whatever the outcome
+    auto drain = [&](int status) {
+        (void)hipStreamSynchronize(st);
+        for (int s = 0; s < kStageSlots; ++s) {
+            pool.wait(&lin[s]);
+            pool.wait(&lout[s]);
+        }
+        return status;
+    };
+    std::vector<const uint8_t*> zin(k);
+    std::vector<uint8_t*> zout(r);
+    hipError_t e;
+    stage_in(0);
+    for (size_t c = 0; c < nchunks; ++c) {
+        const int s = static_cast<int>(c % kStageSlots);
+        const size_t off = c * C, len = std::min(C, sz - off);
+        pool.wait(&lin[s]);   // this chunk's inputs are in the slot
+        pool.wait(&lout[s]);  // the slot's previous outputs have been copied out
+        for (unsigned j = 0; j < k; ++j) zin[j] = base_in[j] + off;
+        for (unsigned i = 0; i < r; ++i) zout[i] = base_out[i] + off;
+        for (size_t q = 0; q < nin; ++q) zin[sin[q]] = ds + s * slot_bytes + q * C;
+        for (size_t q = 0; q < nout; ++q) zout[sout[q]] = ds + s * slot_bytes + (nin + q) * C;
+        if (apply_matrix(coef, k, r, zin.data(), zout.data(), len, 1, 0, 0, st)) return drain(t_status);
+        if ((e = hipEventRecord(d.ev_stg[s], st)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
+        if (c + 1 < nchunks) {
+            // the next slot's inputs were last read by chunk c + 1 - kStageSlots,
+            // synchronised below in an earlier iteration (kStageSlots >= 2)
+            stage_in(c + 1);
+        }
+        if (c >= 1) {
+            const int sp = static_cast<int>((c - 1) % kStageSlots);
+            if ((e = hipEventSynchronize(d.ev_stg[sp])) != hipSuccess)
+                return drain(hip_fail(e, "hipEventSynchronize"));
+            copy_out(c - 1);
+        }
+    }
+    if ((e = hipEventSynchronize(d.ev_stg[(nchunks - 1) % kStageSlots])) != hipSuccess)
+        return drain(hip_fail(e, "hipEventSynchronize"));
+    tr.mark("kernels");
+    copy_out(nchunks - 1);
+    drain(FEC_OK);
+    tr.mark("copy-out");
+    return set_status(FEC_OK);
+}
+
 // Run `coef` (r x k) over in -> out.  Device blocks are used in place; host
 // blocks are staged (small calls: one pinned bounce buffer each way; large
 // calls: the chunked pipeline).  Synchronous unless FEC_FLAG_ASYNC and every
@@ -737,9 +897,13 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     };
     if (m.all_pinned && map_all()) return zero_copy((flags & FEC_FLAG_ASYNC) != 0);
     if (sz * nhost > kPackLimit) {
-        // large pageable blocks: page-lock them for the call and go zero-copy;
-        // the chunked copy pipeline is the fallback when they cannot be mapped
-        if (register_pageable()) {
+        // large pageable blocks: staged through pinned slots by the host
+        // threads (default), or page-locked for the call and accessed in place,
+        // with the chunked copy pipeline as the fallback when they cannot be
+        // mapped
+        const HostPath hp = host_path();
+        if (hp == HostPath::kStage) return run_staged(*d, coef, k, r, in, out, sz, m, st);
+        if (hp == HostPath::kLock && register_pageable()) {
             const int st0 = run_pageable(coef, k, r, in, out, sz, m, st, flags);
             if (st0 != FEC_EAGAIN_INTERNAL) return st0;
         }
