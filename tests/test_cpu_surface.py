@@ -308,3 +308,12 @@ def test_void_entry_points_report_failures(quiet):
     else:
         assert len(enc) == 1 and len(dec) == 1, res.stderr
         assert "status 2" in enc[0] and "no GPU" in enc[0]
+
+
+def test_reuse_host_memory_opt_in():
+    """zfec_amd.reuse_host_memory sets glibc's mmap / trim thresholds (process-wide,
+    opt-in): accepted values return True, and the library keeps
+    working with it (host logic only here, no GPU)."""
+    assert zfec_amd.reuse_host_memory() is True
+    assert zfec_amd.reuse_host_memory(keep_bytes=64 << 20, mmap_threshold=1 << 20) is True
+    assert "reuse_host_memory" in zfec_amd.__all__

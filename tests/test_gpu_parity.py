@@ -244,6 +244,27 @@ def test_c_abi_host_memory_flag():
         assert (rec == data[[0, 2]]).all(), sz
 
 
+@pytest.mark.parametrize("env", [{"ZFEC_HIP_POOL_COPY_MIN": "0"}, {"ZFEC_HIP_STAGE_MIN": str(1 << 60)},
+                                 {"ZFEC_HIP_STAGE_MIN": "0"}])
+def test_host_small_call_paths(env, monkeypatch):
+    """Host calls under 4 MiB: the pinned bounce buffer with its copies on the
+    host pool, the bounce buffer up to 4 MiB (staged path off), and the staged
+    path from any size (blocks >= 64 KiB) -- each bit-exact against the oracle,
+    encode and a mixed primary/secondary decode."""
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    k, m = 3, 10
+    rng = np.random.default_rng(77)
+    for sz in [65536, 70_001, 349_525, 1_000_003]:
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        blocks = [data[i].tobytes() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(blocks)
+        par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+        assert (par == oracle.encode(k, m, data)).all(), sz
+        rec = zfec_amd.Decoder(k, m).decode([out[8], out[1], out[4]], [8, 1, 4])
+        assert rec == blocks, sz
+
+
 def _encode_ptrs_check(code, k, m, data, in_addrs, out_addrs, read_out, sz):
     code.encode_ptrs(in_addrs, out_addrs, list(range(k, m)), sz, flags=0)
     got = read_out()

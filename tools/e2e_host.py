@@ -4,7 +4,9 @@ of one 64 MiB stripe, the path filefec/cmdline_zfec would take.
 
 Strategies timed (GB/s of stripe input bytes, 1e9):
   bytes_api      zfec_amd.Encoder.encode(list of bytes) -> list of bytes
-                 (pageable host buffers; the library stages them)
+                 (pageable host buffers; the library stages them), per call
+                 with the free of the previous call's outputs; then again
+                 after zfec_amd.reuse_host_memory()
   pinned_api     the same C-ABI call with pinned (hipHostMalloc'd) host buffers,
                  e.g. a reader that reads file/socket data straight into pinned
                  memory: the library DMAs them in chunks, overlapping H2D,
@@ -50,18 +52,27 @@ def main():
 
     enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
     out = enc.encode(blocks)
-    # fresh output pages pre-faulted from 4 threads (default) vs faulted by the
-    # page locking itself (ZFEC_HIP_POPULATE=0), interleaved rounds, best of each
-    for rnd in range(3):
-        for tag, val in (("", "1"), ("_nopopulate", "0")):
-            os.environ["ZFEC_HIP_POPULATE"] = val
-            t = timeit(lambda: enc.encode(blocks), 5)
-            key = "bytes_api_encode_GBps" + tag
-            res[key] = max(res.get(key, 0), gbps(k * sz, t))
-            t = timeit(lambda: dec.decode(out[3:6], [3, 4, 5]), 5)
-            key = "bytes_api_decode_GBps" + tag
-            res[key] = max(res.get(key, 0), gbps(k * sz, t))
-    os.environ["ZFEC_HIP_POPULATE"] = "1"
+
+    def bytes_rates(tag):
+        # per call, the free of the previous call's output bytes included (as a
+        # caller sees it), median of 7
+        te, td = [], []
+        for _ in range(7):
+            t0 = time.perf_counter()
+            enc.encode(blocks)
+            t1 = time.perf_counter()
+            dec.decode(out[3:6], [3, 4, 5])
+            td.append(time.perf_counter() - t1)
+            te.append(t1 - t0)
+        res["bytes_api_encode_GBps" + tag] = gbps(k * sz, sorted(te)[3])
+        res["bytes_api_decode_GBps" + tag] = gbps(k * sz, sorted(td)[3])
+
+    # default glibc policy: every call's fresh output pages are faulted in and
+    # returned to the kernel on free
+    bytes_rates("")
+    # zfec_amd.reuse_host_memory(): freed blocks stay in the heap for the next call
+    assert zfec_amd.reuse_host_memory()
+    bytes_rates("_reuse_host_memory")
     assert dec.decode(out[3:6], [3, 4, 5]) == blocks
     assert enc.encode(blocks) == out
 

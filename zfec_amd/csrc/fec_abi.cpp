@@ -347,11 +347,33 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
 
 // Host blocks of up to this many bytes in total go through one pinned bounce
 // buffer (one H2D / D2H each way); larger ones stream through the pipeline.
-constexpr size_t kPackLimit = size_t(4) << 20;
+// From kStageMin bytes, blocks of at least kStageMinBlock bytes take the
+// staged path too: its overlapped copy-in / kernel / copy-out beats the bounce
+// buffer's serial memcpy / DMA / kernel / DMA / memcpy (K=3/M=10 from bytes,
+// 1 MiB stripe: 137 vs 209 us per encode; 256 KiB stripe: 69 vs 77 us), but
+// not for many small blocks (K=20/M=60, 256 KiB stripe of 13 KB blocks: 260
+// vs 122 us; tools/host_lat_ab.py, profiles/r02_host_lat_ab.log).
+// (ZFEC_HIP_PACK_LIMIT / ZFEC_HIP_STAGE_MIN override, read per call for A/B runs.)
+size_t env_size(const char* name, size_t dflt) {
+    const char* e = getenv(name);
+    return e && *e ? static_cast<size_t>(strtoull(e, nullptr, 10)) : dflt;
+}
+size_t pack_limit() { return env_size("ZFEC_HIP_PACK_LIMIT", size_t(4) << 20); }
+size_t stage_min() { return env_size("ZFEC_HIP_STAGE_MIN", size_t(512) << 10); }
+constexpr size_t kStageMinBlock = size_t(64) << 10;
 // Up to this many bytes the kernel accesses the bounce buffer in place.
 constexpr size_t kZeroCopyLimit = size_t(256) << 10;
 // Bytes of each block per pipeline chunk.
 constexpr size_t kPipeChunk = size_t(2) << 20;
+// Small calls: from this many bytes per direction the bounce-buffer copies run
+// on the host pool (ZFEC_HIP_POOL_COPY_MIN, read per call for A/B runs).  Off by
+// default: waking the pool costs more than it saves below 4 MiB (1 MiB
+// K=3/M=10 stripe: 255 us pooled vs 209 us on the calling thread,
+// profiles/r02_host_lat_ab.log).
+size_t pool_copy_min() {
+    const char* e = getenv("ZFEC_HIP_POOL_COPY_MIN");
+    return e && *e ? static_cast<size_t>(strtoull(e, nullptr, 10)) : SIZE_MAX;
+}
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -411,6 +433,21 @@ struct HostTrace {
     std::chrono::steady_clock::time_point t;
     std::string line;
     HostTrace() : on(getenv("ZFEC_HIP_TRACE_HOST") != nullptr), t(std::chrono::steady_clock::now()) {}
+    // accumulated waits inside a loop: lap() starts one, add(i) ends it into slot i
+    std::chrono::steady_clock::time_point l;
+    double acc[3] = {0, 0, 0};
+    void lap() {
+        if (on) l = std::chrono::steady_clock::now();
+    }
+    void add(int i) {
+        if (on) acc[i] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - l).count();
+    }
+    void sums(const char* a, const char* b, const char* c) {
+        if (!on) return;
+        char buf[160];
+        snprintf(buf, sizeof buf, " [%s %.0f %s %.0f %s %.0f]", a, acc[0], b, acc[1], c, acc[2]);
+        line += buf;
+    }
     void mark(const char* what) {
         if (!on) return;
         const auto n = std::chrono::steady_clock::now();
@@ -707,15 +744,19 @@ HostPath host_path() {
 }
 
 // Bytes of every host block per staged chunk: ZFEC_HIP_STAGE_CHUNK, else
-// about 16 MiB of staging per chunk over all host blocks, in whole 64 KiB
+// at most a quarter of the block (so that copy-in, kernel and copy-out of
+// consecutive chunks overlap) and at most about 16 MiB of staging per chunk
+// over all host blocks, in whole 64 KiB
 // (K=3/M=10, 64 MiB from bytes: 8 MiB chunks 8.7 GB/s encode, 16-20 MiB 9.3;
 // 2.5 MiB 6.4; profiles/r02_host_stage_ab.log).
-size_t staged_chunk(size_t nblocks) {
+size_t staged_chunk(size_t nblocks, size_t sz) {
     const char* e = getenv("ZFEC_HIP_STAGE_CHUNK");
     const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0;
     if (v >= (64u << 10)) return static_cast<size_t>(v) / 4096 * 4096;
-    const size_t total = size_t(16) << 20;
-    return std::max<size_t>(256u << 10, total / std::max<size_t>(1, nblocks) / (64u << 10) * (64u << 10));
+    const size_t total = size_t(16) << 20, g = size_t(64) << 10;
+    const size_t by_total = total / std::max<size_t>(1, nblocks) / g * g;
+    const size_t quarter = (sz + 4 * g - 1) / (4 * g) * g;  // at least 4 chunks, so the stages overlap
+    return std::max<size_t>(256u << 10, std::min(by_total, quarter));
 }
 
 int ensure_sbuf(DevCtx& d, size_t bytes) {
@@ -776,7 +817,7 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
         }
     }
     const size_t nin = sin.size(), nout = sout.size();
-    const size_t C = staged_chunk(nin + nout);
+    const size_t C = staged_chunk(nin + nout, sz);
     const size_t slot_bytes = C * (nin + nout);
     if (ensure_sbuf(d, slot_bytes * kStageSlots)) return t_status;
     uint8_t* const hs = static_cast<uint8_t*>(d.sbuf);
@@ -816,8 +857,11 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     for (size_t c = 0; c < nchunks; ++c) {
         const int s = static_cast<int>(c % kStageSlots);
         const size_t off = c * C, len = std::min(C, sz - off);
-        pool.wait(&lin[s]);   // this chunk's inputs are in the slot
+        tr.lap();
+        pool.wait(&lin[s]);  // this chunk's inputs are in the slot
+        tr.add(0);
         pool.wait(&lout[s]);  // the slot's previous outputs have been copied out
+        tr.add(1);
         for (unsigned j = 0; j < k; ++j) zin[j] = base_in[j] + off;
         for (unsigned i = 0; i < r; ++i) zout[i] = base_out[i] + off;
         for (size_t q = 0; q < nin; ++q) zin[sin[q]] = ds + s * slot_bytes + q * C;
@@ -831,7 +875,10 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
         }
         if (c >= 1) {
             const int sp = static_cast<int>((c - 1) % kStageSlots);
-            if ((e = hipEventSynchronize(d.ev_stg[sp])) != hipSuccess)
+            tr.lap();
+            e = hipEventSynchronize(d.ev_stg[sp]);
+            tr.add(2);
+            if (e != hipSuccess)
                 return drain(hip_fail(e, "hipEventSynchronize"));
             copy_out(c - 1);
         }
@@ -839,6 +886,7 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     if ((e = hipEventSynchronize(d.ev_stg[(nchunks - 1) % kStageSlots])) != hipSuccess)
         return drain(hip_fail(e, "hipEventSynchronize"));
     tr.mark("kernels");
+    tr.sums("wait-in", "wait-out", "wait-kernel");
     copy_out(nchunks - 1);
     drain(FEC_OK);
     tr.mark("copy-out");
@@ -896,7 +944,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         return set_status(FEC_OK);
     };
     if (m.all_pinned && map_all()) return zero_copy((flags & FEC_FLAG_ASYNC) != 0);
-    if (sz * nhost > kPackLimit) {
+    if (sz * nhost > pack_limit() || (sz * nhost > stage_min() && sz >= kStageMinBlock)) {
         // large pageable blocks: staged through pinned slots by the host
         // threads (default), or page-locked for the call and accessed in place,
         // with the chunked copy pipeline as the fallback when they cannot be
@@ -922,7 +970,24 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     const size_t nin = m.in_host.size(), nout = m.out_host.size();
     if (ensure_hbuf(*d, slot * (nin + nout))) return t_status;
     uint8_t* hb = static_cast<uint8_t*>(d->hbuf);  // free: the previous call on this thread synchronised
-    for (size_t q = 0; q < nin; ++q) std::memcpy(hb + slot * q, in[m.in_host[q]], sz);
+    // from pool_copy_min() bytes per direction the copies run on the host pool
+    // (256 KiB pieces), below it on this thread
+    const bool pooled = sz * std::max(nin, nout) >= pool_copy_min();
+    auto copy_blocks = [&](bool to_slot) {
+        CopyLatch latch;
+        const size_t n = to_slot ? nin : nout;
+        for (size_t q = 0; q < n; ++q) {
+            uint8_t* sl = hb + slot * (to_slot ? q : nin + q);
+            void* dst = to_slot ? static_cast<void*>(sl) : static_cast<void*>(out[m.out_host[q]]);
+            const void* src = to_slot ? static_cast<const void*>(in[m.in_host[q]]) : static_cast<const void*>(sl);
+            if (pooled)
+                HostPool::get().copy_async(dst, src, sz, &latch, size_t(256) << 10);
+            else
+                std::memcpy(dst, src, sz);
+        }
+        if (pooled) HostPool::get().wait(&latch);
+    };
+    copy_blocks(true);
     if (sz * nhost <= kZeroCopyLimit) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
@@ -941,7 +1006,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
             return hip_fail(e, "hipMemcpyAsync D2H");
     }
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    for (size_t q = 0; q < nout; ++q) std::memcpy(out[m.out_host[q]], hb + slot * (nin + q), sz);
+    copy_blocks(false);
     return set_status(FEC_OK);
 }
 
