@@ -144,3 +144,47 @@ def test_slab_sharded_encode_matches_single_process(world):
     for c0, c1, b in gathered:
         got[:, c0:c1] = np.frombuffer(b, np.uint8).reshape(m - k, c1 - c0)
     assert (got == whole).all()
+
+
+def _barrier_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    import time
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    nb = bench.NodeBarrier(dist, rank, world)
+    assert nb.flags is not None
+    seen = []
+    for i in range(200):
+        if rank == i % world:
+            time.sleep(0.001)  # one late rank per round: nobody may leave before it arrives
+        nb.wait()
+        seen.append(int(nb.flags[:, 0].min()))
+    dist.barrier()
+    q.put((rank, seen == list(range(1, 201)), nb.epoch))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_barrier_shared_memory(world):
+    """bench.py's NodeBarrier (shared-memory spin barrier bracketing the timed
+    steps): no rank leaves a round before every rank has arrived at it, over
+    200 rounds with a different late rank each round; the backing file is
+    unlinked after set-up."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_barrier_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r for r, _, _ in res) == list(range(world))
+    assert all(ok and epoch == 200 for _, ok, epoch in res)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("zfec_bench_barrier_")]
