@@ -133,7 +133,7 @@ class NodeBarrier:
     def __init__(self, dist, rank, world):
         self.world, self.rank, self.epoch, self.flags = world, rank, 0, None
         if dist is None or world == 1 or os.environ.get("ZFEC_BENCH_BARRIER") == "dist":
-            self.dist = dist
+            self.dist = dist if world > 1 else None
             return
         import mmap
         import uuid
