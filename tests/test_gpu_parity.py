@@ -907,3 +907,40 @@ def test_large_pageable_bytes_path(path, chunk, monkeypatch):
     assert b"".join(dec) == flat.tobytes()
     sub = zfec_amd.Encoder(k, m).encode([v.tobytes() for v in views], [9, 4])
     assert sub[0] == out[9] and sub[1] == out[4]
+
+
+def test_staged_host_path_concurrent_threads():
+    """Several Python threads (the GIL is released in the call) run large
+    host-memory encodes and decodes at once: every call's chunks go through
+    its own thread's pinned staging slots while all of them share one host
+    copy pool (fec_abi.cpp run_staged, host_pool.cpp).  Bit-exact against the
+    oracle, K=3/M=10 and K=20/M=60, sizes that cut the last chunk short."""
+    import threading
+
+    cases = [(3, 10, (3 << 20) + 17), (20, 60, (256 << 10) + 3), (3, 10, 700_001), (10, 16, (1 << 20) + 5)]
+    rng = np.random.default_rng(2024)
+    inputs = [rng.integers(0, 256, size=(k, sz), dtype=np.uint8) for k, m, sz in cases]
+    want = [oracle.encode(k, m, d) for (k, m, sz), d in zip(cases, inputs)]
+    errors = []
+
+    def work(i):
+        try:
+            k, m, sz = cases[i % len(cases)]
+            data = inputs[i % len(cases)]
+            blocks = [data[j].tobytes() for j in range(k)]
+            for _ in range(3):
+                out = zfec_amd.Encoder(k, m).encode(blocks)
+                par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+                assert (par == want[i % len(cases)]).all(), (i, k, m, sz)
+                nums = list(range(m - k, m))
+                assert zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums) == blocks, (i, k, m, sz)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ths)
+    assert not errors, errors
