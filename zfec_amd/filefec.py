@@ -3,7 +3,9 @@
 Mirrors /root/reference/zfec/filefec.py: the 1-4 byte bit-packed header
 (`_build_header` :58-118, `_parse_header` :123-181), `encode_to_files`
 (:185-256), `decode_from_files` (:264-316) and the segment callback API
-`encode_file_stringy_easyfec` (:494-522).  Share files are byte-identical to
+(`encode_file` :318-375, `encode_file_not_really` :385-414,
+`encode_file_not_really_and_hash` :416-448, `encode_file_stringy` :450-492,
+`encode_file_stringy_easyfec` :494-522).  Share files are byte-identical to
 the reference's (tests/test_filefec.py checks them against files written by
 the reference itself).
 
@@ -381,6 +383,129 @@ def decode_from_files(outf, infiles, verbose=False):
     if verbose:
         print()
         print("Done!")
+
+
+def _segments(inf, k, m, chunksize):
+    """Whole segments of k*chunksize input bytes, encoded a window at a time:
+    the window is read into page-locked memory and ONE batched GPU call
+    (fec_encode_batch, stripe = segment) computes the parity of all its full
+    segments.  Yields (window bytes, offset of the segment, parity rows,
+    offset of its parity) per full segment in file order, then
+    (tail bytes, None, None, None) once for the final short segment -- empty
+    when the file is a whole number of segments, as the reference's loops
+    (filefec.py:352-375, :473-492) also end on a segment they pad entirely."""
+    seg = k * chunksize
+    r = m - k
+    wseg = max(1, WINDOW_BYTES // seg)
+    code = capi.Code(k, m)
+    win_in, rows = _PinnedArray(wseg * seg), _PinnedArray(max(1, r) * wseg * chunksize)
+    try:
+        while True:
+            got = _readinto_full(inf, memoryview(win_in.array)[:wseg * seg])
+            nfull = got // seg
+            if nfull and r:
+                code.encode_batch(win_in.ptr, chunksize, seg, rows.ptr, chunksize, r * chunksize, list(range(k, m)),
+                                  chunksize, nfull, flags=capi.FEC_FLAG_LIBRARY_STREAM)
+            win = win_in.array[:nfull * seg].tobytes()
+            par = rows.array[:nfull * r * chunksize].tobytes()
+            for s in range(nfull):
+                yield win, s * seg, par, s * r * chunksize
+            if got < wseg * seg:
+                yield bytes(win_in.array[nfull * seg:got]), None, None, None
+                return
+    finally:
+        win_in.free()
+        rows.free()
+
+
+def _segment_results(k, m, chunksize, win, off, par, poff, blocks):
+    """cb's first argument: the k input blocks (`blocks`, filled from the
+    segment) followed by the m - k parity blocks as bytes."""
+    for j in range(k):
+        blocks[j][:] = win[off + j * chunksize:off + (j + 1) * chunksize]
+    return list(blocks) + [par[poff + i * chunksize:poff + (i + 1) * chunksize] for i in range(m - k)]
+
+
+def encode_file(inf, cb, k, m, chunksize=4096):
+    """Segment callback API (filefec.py:318-375): read k blocks of chunksize
+    bytes at a time, encode them into m blocks, call cb(blocks, indatasize).
+    The first k items of `blocks` are mutable arrays (bytearray) whose contents
+    the next segment overwrites; the rest are new bytes.  indatasize is
+    k*chunksize except for the final segment, which is zero-padded and carries
+    the number of real bytes in it (0 when the file length is a multiple of
+    k*chunksize).  The reference builds its arrays with the Python 2 typecode
+    'c', which Python 3 rejects; this keeps the documented behaviour."""
+    enc = zfec_amd.Encoder(k, m)
+    blocks = tuple(bytearray(chunksize) for _ in range(k))
+    for win, off, par, poff in _segments(inf, k, m, chunksize):
+        if off is not None:
+            cb(_segment_results(k, m, chunksize, win, off, par, poff, blocks), k * chunksize)
+            continue
+        padded = win + b"\x00" * (k * chunksize - len(win))
+        for j in range(k):
+            blocks[j][:] = padded[j * chunksize:(j + 1) * chunksize]
+        res = enc.encode(list(blocks))
+        cb(list(blocks) + list(res[k:]), len(win))
+
+
+def encode_file_stringy(inf, cb, k, m, chunksize=4096):
+    """Segment callback API with bytes blocks (filefec.py:450-492): as
+    encode_file, with the k input blocks as bytes.  The final segment's
+    indatasize is what the reference reports: i*chunksize + len(last read),
+    with i counting the short read itself (one chunksize more than the real
+    byte count; chunksize for an all-padding final segment); pinned against
+    the reference's own callback sequences (tests/golden/segments.json)."""
+    enc = zfec_amd.Encoder(k, m)
+    for win, off, par, poff in _segments(inf, k, m, chunksize):
+        if off is not None:
+            blocks = [win[off + j * chunksize:off + (j + 1) * chunksize] for j in range(k)]
+            cb(blocks + [par[poff + i * chunksize:poff + (i + 1) * chunksize] for i in range(m - k)], k * chunksize)
+            continue
+        i = len(win) // chunksize + 1  # the read that came back short, counted from 1
+        padded = win + b"\x00" * (k * chunksize - len(win))
+        blocks = [padded[j * chunksize:(j + 1) * chunksize] for j in range(k)]
+        ind = i * chunksize + len(win) % chunksize
+        cb(enc.encode(blocks), ind)
+        if ind == k * chunksize and win:
+            # (k-1)*chunksize bytes left: the reference's loop condition still
+            # holds, so it reads once more and reports an all-padding segment
+            # of "chunksize" bytes.  (With k == 1 and an empty tail its loop
+            # never ends; here the stream ends.)
+            blocks = [b"\x00" * chunksize] * k
+            cb(enc.encode(blocks), chunksize)
+
+
+def encode_file_not_really(inf, cb, k, m, chunksize=4096):
+    """Benchmark control (filefec.py:385-414): read and pad segments as
+    encode_file does, encode nothing, call cb(None, None) per segment."""
+    for _ in _segments_read_only(inf, k, chunksize):
+        cb(None, None)
+
+
+def encode_file_not_really_and_hash(inf, cb, k, m, chunksize=4096):
+    """Benchmark control (filefec.py:416-448): as encode_file_not_really, and
+    SHA-1 every padded input block (the reference's `sha1.new()` is Python 2)."""
+    import hashlib
+
+    hasher = hashlib.sha1()
+    for blocks in _segments_read_only(inf, k, chunksize):
+        for b in blocks:
+            hasher.update(b)
+        cb(None, None)
+    return hasher.hexdigest()
+
+
+def _segments_read_only(inf, k, chunksize):
+    """The padded k blocks of every segment, read without encoding (the final,
+    possibly all-padding segment included)."""
+    seg = k * chunksize
+    while True:
+        data = inf.read(seg)
+        if len(data) < seg:
+            data = data + b"\x00" * (seg - len(data))
+            yield [data[j * chunksize:(j + 1) * chunksize] for j in range(k)]
+            return
+        yield [data[j * chunksize:(j + 1) * chunksize] for j in range(k)]
 
 
 def encode_file_stringy_easyfec(inf, cb, k, m, chunksize=4096):
