@@ -317,3 +317,13 @@ def test_reuse_host_memory_opt_in():
     assert zfec_amd.reuse_host_memory() is True
     assert zfec_amd.reuse_host_memory(keep_bytes=64 << 20, mmap_threshold=1 << 20) is True
     assert "reuse_host_memory" in zfec_amd.__all__
+
+
+def test_package_exports_like_reference():
+    """`import zfec` makes Encoder, Decoder, Error, __version__ and the modules
+    easyfec, filefec, cmdline_zfec, cmdline_zunfec available
+    (/root/reference/zfec/__init__.py); so does `import zfec_amd`."""
+    for name in ["Encoder", "Decoder", "Error", "__version__", "easyfec", "filefec", "cmdline_zfec",
+                 "cmdline_zunfec"]:
+        assert hasattr(zfec_amd, name), name
+    assert issubclass(zfec_amd.filefec.CorruptedShareFilesError, zfec_amd.Error)

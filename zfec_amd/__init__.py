@@ -22,7 +22,8 @@ from ._fec import Error, device_count, test_from_agl, version
 
 __version__ = "0.1.0"
 
-__all__ = ["Encoder", "Decoder", "Error", "easyfec", "test_from_agl", "device_count", "version", "reuse_host_memory"]
+__all__ = ["Encoder", "Decoder", "Error", "easyfec", "filefec", "cmdline_zfec", "cmdline_zunfec", "test_from_agl",
+           "device_count", "version", "reuse_host_memory"]
 
 
 def _is_device_tensor(x):
@@ -288,6 +289,7 @@ class Decoder(_fec.Decoder):
 
 
 from . import easyfec  # noqa: E402  (needs Encoder/Decoder above)
+from . import filefec, cmdline_zfec, cmdline_zunfec  # noqa: E402  (as zfec/__init__.py imports them)
 
 
 def reuse_host_memory(keep_bytes=1 << 30, mmap_threshold=32 << 20):
