@@ -30,11 +30,12 @@ def need_gpu():
 @pytest.fixture(params=[("2", "0", "0"), ("4", "0", "0"), ("2", "1", "0"), ("2", "0", "1")],
                 ids=["phase2", "phase4", "phase2_sb", "phase2_bb"])
 def bsg_only(request):
-    """JIT off, generic kernel on; the variant knobs are read per launch."""
+    """JIT off, generic kernel on, matapply_small off (these small launches
+    would take it); the variant knobs are read per launch."""
     prev_j, prev_g = capi.jit_mode(capi.JIT_OFF), capi.generic_mode(1)
-    keys = ("ZFEC_HIP_BSG_PHASE", "ZFEC_HIP_BSG_SB", "ZFEC_HIP_BSG_BB")
+    keys = ("ZFEC_HIP_BSG_PHASE", "ZFEC_HIP_BSG_SB", "ZFEC_HIP_BSG_BB", "ZFEC_HIP_SMALL_LANES")
     old = {key: os.environ.get(key) for key in keys}
-    os.environ.update(dict(zip(keys, request.param)))
+    os.environ.update(dict(zip(keys, tuple(request.param) + ("0",))))
     yield
     for key, val in old.items():
         if val is None:
@@ -138,7 +139,7 @@ def test_bsg_fresh_erasure_patterns(bsg_only):
 
 def test_bsg_off_gives_identical_bytes():
     """generic mode off: the table kernels serve the same launch, same bytes."""
-    k, m, sz = 20, 60, 70000
+    k, m, sz = 20, 60, 70000  # 8750 eight-byte units: past matapply_small's threshold
     rng = np.random.default_rng(5)
     data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
     ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]

@@ -944,3 +944,49 @@ def test_staged_host_path_concurrent_threads():
         t.join(timeout=240)
     assert not any(t.is_alive() for t in ths)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("k,m", [(5, 9), (10, 16), (20, 60), (32, 80), (40, 50), (4, 16), (12, 13), (200, 256)])
+def test_small_launch_kernel_vs_oracle(k, m):
+    """Launches too small for the unit kernels (a wave per output row,
+    matapply_small): device blocks of 1, 3, 4, 5, 205, 4097 and 16000 bytes,
+    encode and a decode from the last k blocks, bit-exact against the oracle;
+    k > 32 takes the XOR-accumulating continuation launches."""
+    rng = np.random.default_rng(k * 1000 + m)
+    for sz in (1, 3, 4, 5, 205, 4097, 16000):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        if not (k <= 4 and m - k <= 8):
+            assert capi.last_kernel_name() == "matapply_small", (k, m, sz, capi.last_kernel_name())
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        nums = list(range(m - k, m))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz)
+
+
+def test_small_launch_kernel_batched_strided():
+    """matapply_small over a batch of stripes at odd strides and misaligned
+    bases; bytes between rows and after the last one stay 0xA5."""
+    k, m, sz, ns = 20, 60, 333, 5
+    r = m - k
+    rng = np.random.default_rng(333)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    ld = sz + 13
+    base_in, base_out = 1, 7
+    src = torch.zeros(base_in + ns * k * ld, dtype=torch.uint8, device="cuda")
+    src[base_in:].view(ns, k, ld)[:, :, :sz] = torch.from_numpy(data).cuda()
+    dst = torch.full((base_out + ns * r * ld + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    code.encode_batch(src.data_ptr() + base_in, ld, k * ld, dst.data_ptr() + base_out, ld, r * ld,
+                      list(range(k, m)), sz, ns, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name() == "matapply_small", capi.last_kernel_name()
+    d = dst.cpu().numpy()
+    assert (d[:base_out] == 0xA5).all() and (d[base_out + ns * r * ld:] == 0xA5).all()
+    out = d[base_out:base_out + ns * r * ld].reshape(ns, r, ld)
+    assert (out[:, :, sz:] == 0xA5).all(), "write past a row"
+    for s in range(ns):
+        assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s

@@ -988,7 +988,15 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         if (pooled) HostPool::get().wait(&latch);
     };
     copy_blocks(true);
-    if (sz * nhost <= kZeroCopyLimit) {
+    // Zero-copy only for the register kernels (k <= 4, r <= 8), which issue
+    // all their input loads at once: the wide-code kernels read inputs in
+    // groups, each group a PCIe round trip of its own (K=20/M=60, 4 KiB stripe:
+    // 40 us in the kernel over PCIe; tools/small_call_probe.py under
+    // rocprofv3, profiles/r02_small_calls.log).  ZFEC_HIP_ZC_WIDE=1 keeps
+    // them zero-copy (A/B runs).
+    const char* zcw = getenv("ZFEC_HIP_ZC_WIDE");
+    const bool zc_kernel = (k <= 4 && r <= 8) || (zcw && zcw[0] == '1');
+    if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = hbd + slot * (nin + q);

@@ -940,6 +940,110 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
 }
 
 // ---------------------------------------------------------------------------
+// matapply_small: launches too small to fill the chip with the unit kernels,
+// for codes beyond the register kernels (k > 4 or r > 8).  The unit kernels
+// give each lane every output row of its slice: a K=20/M=60 stripe of 4 KiB
+// (205-byte blocks) is 26 lanes doing 800 coefficient MACs each, ~30-40 us
+// in one wave (tools/small_call_probe.py under rocprofv3,
+// profiles/r02_small_calls.log).  Here a wave owns one output row (so its
+// coefficients are wave-uniform: their tables are scalar loads from the
+// bank) and 64 four-byte units of it, and each lane does k MACs with all k
+// input loads in flight at once.  Inputs are re-read once per row, from L2
+// (host calls stage wide codes through device memory, fec_abi.cpp).  Python
+// bytes calls, K=20/M=60: 4 KiB stripe 57-59 -> 25-26 us per encode, 64 KiB
+// 77-81 -> 43-52, 256 KiB 111-121 -> 68-79 (profiles/r02_small_calls.log).
+// Launch: gs_c = waves per row, gs_s = bytes per unit (4, or 1 when sz < 4),
+// cps = units per stripe.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void matapply_small(const MatJob job) {
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wpr = job.gs_c;
+    const uint32_t row = __builtin_amdgcn_readfirstlane(wave / wpr);
+    if (row >= job.r) return;
+    const uint64_t unit = uint64_t(wave - row * wpr) * 64u + (threadIdx.x & 63u);
+    const uint64_t cps = job.cps;
+    if (unit >= cps * job.nstripes) return;
+    const uint32_t ub = job.gs_s;
+    const uint64_t s = unit / cps;
+    uint64_t off = (unit - s * cps) * ub;
+    // The last unit of a block: shifted back to end at sz (its neighbour
+    // stores the same bytes), except when accumulating, where two lanes of
+    // different waves would both read-modify-write the overlap: there it
+    // takes only its own bytes (nb < 4), one at a time.
+    uint32_t nb = ub;
+    if (off + ub > job.sz) {
+        if (job.accumulate)
+            nb = static_cast<uint32_t>(job.sz - off);
+        else
+            off = job.sz - ub;
+    }
+    const uint64_t io = s * job.in_sstride + off, oo = s * job.out_sstride + off;
+    uint32_t acc = 0;
+    if (nb == 4u) {
+        // every input load is issued before the first is used: one memory
+        // latency per launch instead of one per input
+        uint32_t xs[kMaxIn];
+#pragma unroll
+        for (uint32_t j = 0; j < static_cast<uint32_t>(kMaxIn); ++j)
+            if (j < job.k) __builtin_memcpy(&xs[j], job.in[j] + io, 4);
+#pragma unroll
+        for (uint32_t j = 0; j < static_cast<uint32_t>(kMaxIn); ++j) {
+            if (j < job.k) {
+                const uint32_t* t = &g_bank.w[uint32_t(job.coef[row * job.k + j]) * 8u];
+                const Sel sl = selectors(xs[j]);
+                acc = xor3(acc, perm(t[1], t[0], sl.s0), perm(t[3], t[2], sl.s1)) ^ perm(t[4], t[4], sl.s2);
+            }
+        }
+    } else {  // the bytes of a block shorter than 4, or an accumulating launch's tail
+        for (uint32_t j = 0; j < job.k; ++j) {
+            uint32_t x = 0;
+            for (uint32_t q = 0; q < nb; ++q) x |= uint32_t(job.in[j][io + q]) << (8 * q);
+            const uint32_t* t = &g_bank.w[uint32_t(job.coef[row * job.k + j]) * 8u];
+            const Sel sl = selectors(x);
+            acc = xor3(acc, perm(t[1], t[0], sl.s0), perm(t[3], t[2], sl.s1)) ^ perm(t[4], t[4], sl.s2);
+        }
+    }
+    uint8_t* op = job.out[row] + oo;
+    if (nb == 4u) {
+        if (job.accumulate) {
+            uint32_t o;
+            __builtin_memcpy(&o, op, 4);
+            acc ^= o;
+        }
+        __builtin_memcpy(op, &acc, 4);
+    } else {
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint8_t v = static_cast<uint8_t>(acc >> (8 * b));
+            op[b] = job.accumulate ? static_cast<uint8_t>(op[b] ^ v) : v;
+        }
+    }
+}
+
+// Launches whose unit kernels would run fewer lanes than this take
+// matapply_small (ZFEC_HIP_SMALL_LANES overrides, read per launch; 0 turns it
+// off).
+uint64_t small_lanes() {
+    const char* e = getenv("ZFEC_HIP_SMALL_LANES");
+    return e && *e ? strtoull(e, nullptr, 10) : 2048ull;
+}
+
+hipError_t launch_small(MatJob& job, hipStream_t stream) {
+    const uint32_t ub = job.sz >= 4 ? 4u : 1u;
+    const uint64_t cps = (job.sz + ub - 1) / ub;
+    const uint64_t units = cps * job.nstripes;
+    const uint64_t wpr = (units + 63) / 64;
+    const uint64_t waves = wpr * job.r;
+    if (waves > (1ull << 31)) return hipErrorNotSupported;
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_c = static_cast<uint32_t>(wpr);
+    job.gs_s = ub;
+    job.xcd_swizzle = 0;
+    const uint32_t grid = static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64));
+    hipLaunchKernelGGL(matapply_small, dim3(grid), dim3(kBlock), 0, stream, job);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Dispatch
 // ---------------------------------------------------------------------------
 typedef void (*KernelFn)(const MatJob);
@@ -1182,6 +1286,14 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
             return hipSuccess;
         }
         if (je != hipErrorNotSupported && je != hipErrorNotReady) return je;
+    }
+    if (!job.tables && !(job.k <= static_cast<uint32_t>(kRegK) && job.r <= static_cast<uint32_t>(kRegR)) &&
+        (job.sz + 7) / 8 * job.nstripes < small_lanes()) {
+        const hipError_t se = launch_small(job, stream);
+        if (se != hipErrorNotSupported) {
+            t_last_kernel = "matapply_small";
+            return se;
+        }
     }
     if (bsg_eligible(job)) {
         const hipError_t be = launch_bsg(job, stream);
