@@ -122,7 +122,10 @@ int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts
                   const unsigned* index, size_t sz, void* stream, unsigned flags);
 
 /* Batched encode of nstripes independent stripes in one launch (device memory
- * on one device, or page-locked host memory).  Block j of stripe s is read from src + s*src_stripe_stride +
+ * on one device, or page-locked host memory).  Pageable host memory on either
+ * side is accepted too: it is staged through pinned slots in groups of stripes
+ * by the library's host threads (only the rows are written; the call is then
+ * synchronous and FEC_FLAG_ROW_PADDING does not apply).  Block j of stripe s is read from src + s*src_stripe_stride +
  * j*src_block_stride; output i of stripe s (block block_nums[i]) is written to
  * dst + s*dst_stripe_stride + i*dst_block_stride.  Packed [stripe][block][sz]
  * layouts use block_stride = sz, stripe_stride = k*sz (input) / num*sz (output).

@@ -990,3 +990,75 @@ def test_small_launch_kernel_batched_strided():
     assert (out[:, :, sz:] == 0xA5).all(), "write past a row"
     for s in range(ns):
         assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s
+
+
+@pytest.mark.parametrize("layout", ["packed", "padded_rows", "block_major", "src_device", "dst_device"])
+def test_batch_pageable_host_memory(layout):
+    """fec_encode_batch / fec_decode_batch on pageable host memory (numpy):
+    staged through pinned slots in groups of stripes (fec_abi.cpp
+    run_batch_staged).  Object-major packed rows, rows padded with guard bytes
+    that must stay untouched, block-major arrays, and one side on the device;
+    enough stripes for several groups; parity and decode vs the oracle."""
+    k, m, sz, ns = 5, 12, 3001, 2000
+    r = m - k
+    rng = np.random.default_rng(ns + sz)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    code = capi.Code(k, m)
+    pad = 37 if layout == "padded_rows" else 0
+    ld = sz + pad
+    if layout == "block_major":
+        src = np.ascontiguousarray(data.transpose(1, 0, 2))  # [k][ns][sz]
+        sptr, sbs, sss = src.ctypes.data, ns * sz, sz
+        dst = np.full((r, ns, sz), 0xA5, np.uint8)
+        dptr, dbs, dss = dst.ctypes.data, ns * sz, sz
+        read_par = lambda: dst.transpose(1, 0, 2)
+    else:
+        src = np.full((ns, k, ld), 0x5A, np.uint8)
+        src[:, :, :sz] = data
+        dst = np.full((ns, r, ld), 0xA5, np.uint8)
+        sptr, sbs, sss = src.ctypes.data, ld, k * ld
+        dptr, dbs, dss = dst.ctypes.data, ld, r * ld
+        read_par = lambda: dst[:, :, :sz]
+    keep = []
+    if layout == "src_device":
+        t = torch.from_numpy(src).cuda()
+        keep.append(t)
+        sptr = t.data_ptr()
+    dev_out = None
+    if layout == "dst_device":
+        dev_out = torch.full(dst.shape, 0xA5, dtype=torch.uint8, device="cuda")
+        dptr = dev_out.data_ptr()
+    code.encode_batch(sptr, sbs, sss, dptr, dbs, dss, list(range(k, m)), sz, ns, flags=capi.FEC_FLAG_LIBRARY_STREAM)
+    torch.cuda.synchronize()
+    if dev_out is not None:
+        dst[...] = dev_out.cpu().numpy()
+    par = read_par()
+    for s in list(range(0, ns, 97)) + [ns - 1]:
+        assert (par[s] == oracle.encode(k, m, data[s])).all(), (layout, s)
+    if pad:
+        assert (dst[:, :, sz:] == 0xA5).all(), "a padded row's guard bytes were written"
+    # decode every stripe from parity blocks 5..9 (all primaries missing)
+    nums = list(range(k, 2 * k))
+    recv = np.ascontiguousarray(par[:, :k, :])  # slots hold blocks k..2k-1
+    rec = np.full((ns, k, sz), 0x33, np.uint8)
+    code.decode_batch(recv.ctypes.data, sz, k * sz, rec.ctypes.data, sz, k * sz, nums, sz, ns,
+                      flags=capi.FEC_FLAG_LIBRARY_STREAM)
+    assert (rec == data).all(), layout
+
+
+def test_batch_api_host_numpy_arrays():
+    """Encoder.encode_batch / Decoder.decode_batch take host numpy arrays too
+    (object-major and transposed block-major), results as numpy arrays."""
+    k, m, sz, ns = 3, 10, 1366, 5000
+    rng = np.random.default_rng(1366)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+    for blocks in (data, np.ascontiguousarray(data.transpose(1, 0, 2)).transpose(1, 0, 2)):
+        par = enc.encode_batch(blocks)
+        assert isinstance(par, np.ndarray) and par.shape == (ns, m - k, sz)
+        for s in (0, 1, 2500, ns - 1):
+            assert (par[s] == oracle.encode(k, m, data[s])).all(), s
+        nums = [7, 1, 9]
+        recv = np.stack([par[:, 4], data[:, 1], par[:, 6]], axis=1)
+        rec = dec.decode_batch(recv, nums)
+        assert (rec == data[:, [0, 2], :]).all()

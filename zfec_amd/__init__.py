@@ -67,31 +67,73 @@ def _device_blocks(blocks, k):
     return bl, sz, dev
 
 
-def _batch_view(blocks, nblocks, what):
-    """Check a [nstripes, nblocks, sz] uint8 device tensor for the batched entry
-    points; any strides with unit stride along sz, so a transposed block-major
-    [nblocks, nstripes, sz] array passes as is (fec_encode_batch runs it as one
-    long stripe).  Returns (nstripes, sz, block stride, stripe stride)."""
-    import torch
+def _is_host_array(x):
+    return type(x).__module__ == "numpy" and hasattr(x, "ctypes")
 
-    if not _is_device_tensor(blocks) or blocks.dtype != torch.uint8 or blocks.dim() != 3:
-        raise Error("Precondition violation: %s is required to be a uint8 device tensor [nstripes, %d, sz]"
-                    % (what, nblocks))
-    ns, nb, sz = blocks.shape
+
+def _batch_view(blocks, nblocks, what):
+    """Check a [nstripes, nblocks, sz] uint8 array for the batched entry points:
+    a device tensor, or a host numpy array (pageable memory; the library stages
+    it through pinned slots, fec_abi.cpp run_batch_staged).  Any strides with
+    unit stride along sz, so a transposed block-major [nblocks, nstripes, sz]
+    array passes as is (fec_encode_batch runs it as one long stripe).
+    Returns (nstripes, sz, block stride, stripe stride, data pointer)."""
+    if _is_host_array(blocks):
+        import numpy as np
+
+        if blocks.dtype != np.uint8 or blocks.ndim != 3:
+            raise Error("Precondition violation: %s is required to be a uint8 array [nstripes, %d, sz]"
+                        % (what, nblocks))
+        ns, nb, sz = blocks.shape
+        strides = blocks.strides
+        ptr = blocks.ctypes.data
+    else:
+        import torch
+
+        if not _is_device_tensor(blocks) or blocks.dtype != torch.uint8 or blocks.dim() != 3:
+            raise Error("Precondition violation: %s is required to be a uint8 device tensor or numpy array "
+                        "[nstripes, %d, sz]" % (what, nblocks))
+        ns, nb, sz = blocks.shape
+        strides = (blocks.stride(0), blocks.stride(1), blocks.stride(2))
+        ptr = blocks.data_ptr()
     if nb != nblocks:
         raise Error("Precondition violation: %s is required to hold %d blocks per stripe, not %d" % (what, nblocks, nb))
-    if sz > 1 and blocks.stride(2) != 1:
+    if sz > 1 and strides[2] != 1:
         raise Error("Precondition violation: %s blocks are required to be contiguous along sz" % what)
-    return ns, sz, blocks.stride(1), blocks.stride(0)
+    if min(strides[0], strides[1]) < 0:
+        raise Error("Precondition violation: %s is required to have non-negative strides" % what)
+    return ns, sz, strides[1], strides[0], ptr
 
 
-def _batch_out(like_block_major, ns, nb, sz, device):
-    """Output tensor [ns, nb, sz]: block-major storage when the input was."""
+def _batch_out(like, like_block_major, ns, nb, sz):
+    """Output [ns, nb, sz] where `like` lives (device tensor or numpy array):
+    block-major storage when the input was."""
+    shape = (nb, ns, sz) if like_block_major else (ns, nb, sz)
+    if _is_host_array(like):
+        import numpy as np
+
+        out = np.empty(shape, dtype=np.uint8)
+        return out.transpose(1, 0, 2) if like_block_major else out
     import torch
 
-    if like_block_major:
-        return torch.empty((nb, ns, sz), dtype=torch.uint8, device=device).transpose(0, 1)
-    return torch.empty((ns, nb, sz), dtype=torch.uint8, device=device)
+    out = torch.empty(shape, dtype=torch.uint8, device=like.device)
+    return out.transpose(0, 1) if like_block_major else out
+
+
+def _batch_strides(out):
+    if _is_host_array(out):
+        return out.ctypes.data, out.strides[1], out.strides[0]
+    return out.data_ptr(), out.stride(1), out.stride(0)
+
+
+def _batch_call_args(blocks):
+    """stream / flags of a batched call: a device tensor's work is enqueued on
+    its current stream; host arrays are synchronous."""
+    from . import capi
+
+    if _is_host_array(blocks):
+        return 0, capi.FEC_FLAG_LIBRARY_STREAM
+    return _stream_handle(blocks.device), capi.FEC_FLAG_ASYNC
 
 
 class _as_error(object):
@@ -137,10 +179,11 @@ class Encoder(_fec.Encoder):
 
         blocks: uint8 device tensor [nstripes, k, sz] (any strides with unit
         stride along sz; a transposed block-major [k, nstripes, sz] array is the
-        fastest layout).  desired_blocks_nums: secondary block numbers in
-        [k, m-1] (default k..m-1).  Returns a new [nstripes, len(desired), sz]
-        tensor, block-major when the input was; work is enqueued on the current
-        stream.  A batched counterpart of encode() for many small objects
+        fastest layout), or the same as a host numpy array.  desired_blocks_nums:
+        secondary block numbers in [k, m-1] (default k..m-1).  Returns a new
+        [nstripes, len(desired), sz] tensor (numpy array for host input),
+        block-major when the input was; device work is enqueued on the current
+        stream, host calls return when done.  A batched counterpart of encode() for many small objects
         (SURVEY.md §8f row 2); no reference equivalent."""
         from . import capi
 
@@ -150,13 +193,13 @@ class Encoder(_fec.Encoder):
             if not isinstance(x, int) or x < k or x >= m:
                 raise Error("Precondition violation: encode_batch desired block nums are required to be secondary "
                             "block nums in [k, m-1] = [%d, %d], but one was %r" % (k, m - 1, x))
-        ns, sz, sbs, sss = _batch_view(blocks, k, "blocks")
-        out = _batch_out(sss < sbs, ns, len(nums), sz, blocks.device)
+        ns, sz, sbs, sss, ptr = _batch_view(blocks, k, "blocks")
+        out = _batch_out(blocks, sss < sbs, ns, len(nums), sz)
         if nums and ns and sz:
+            optr, obs, oss = _batch_strides(out)
+            stream, flags = _batch_call_args(blocks)
             with _as_error():
-                _capi_code(self).encode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1),
-                                              out.stride(0), nums, sz, ns, stream=_stream_handle(blocks.device),
-                                              flags=capi.FEC_FLAG_ASYNC)
+                _capi_code(self).encode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream, flags=flags)
         return out
 
     def _encode_device(self, inblocks, desired):
@@ -205,8 +248,9 @@ class Decoder(_fec.Decoder):
         """Decode many independent stripes that all received the same block
         numbers, in one launch (fec_decode_batch).
 
-        blocks: uint8 device tensor [nstripes, k, sz] (strides as in
-        Encoder.encode_batch), slot j of every stripe holding block blocknums[j];
+        blocks: uint8 device tensor or host numpy array [nstripes, k, sz]
+        (strides as in Encoder.encode_batch), slot j of every stripe holding
+        block blocknums[j];
         a primary block must sit at its own slot (primary i at slot i, as
         fec_decode requires, zfec/fec.c:549).  Returns a new [nstripes, r, sz]
         tensor of the r missing primaries in ascending order."""
@@ -225,14 +269,14 @@ class Decoder(_fec.Decoder):
                             "was %r" % (m - 1, x))
             if x < k and x != i:
                 raise Error("Precondition violation: decode_batch requires primary block %d at slot %d" % (x, x))
-        ns, sz, sbs, sss = _batch_view(blocks, k, "blocks")
+        ns, sz, sbs, sss, ptr = _batch_view(blocks, k, "blocks")
         r = sum(1 for x in nums if x >= k)
-        out = _batch_out(sss < sbs, ns, r, sz, blocks.device)
+        out = _batch_out(blocks, sss < sbs, ns, r, sz)
         if r and ns and sz:
+            optr, obs, oss = _batch_strides(out)
+            stream, flags = _batch_call_args(blocks)
             with _as_error():
-                _capi_code(self).decode_batch(blocks.data_ptr(), sbs, sss, out.data_ptr(), out.stride(1),
-                                              out.stride(0), nums, sz, ns, stream=_stream_handle(blocks.device),
-                                              flags=capi.FEC_FLAG_ASYNC)
+                _capi_code(self).decode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream, flags=flags)
         return out
 
     def _check_blocknums(self, blocknums):

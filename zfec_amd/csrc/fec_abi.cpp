@@ -893,6 +893,145 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     return set_status(FEC_OK);
 }
 
+// Batched calls on pageable host memory (fec_encode_batch / fec_decode_batch
+// with a src or dst the GPU cannot address), staged like run_staged but cut
+// into groups of whole stripes: the host pool copies a group's input rows
+// into a pinned slot, one batched launch runs the group on the slot, and the
+// pool copies the output rows out -- only the rows, so bytes between rows
+// and past sz in the caller's arrays are never written.  In the slot a
+// group's rows are packed [stripe][block][sz], or [block][stripe][sz] when the
+// caller's side is block-major (stripe stride == sz), which keeps the
+// block-major launch shape.  A side in device or page-locked memory is used
+// in place (`src` / `dst` are then kernel-visible addresses).
+int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* src, size_t sbs, size_t sss,
+                     bool src_host, gf* dst, size_t dbs, size_t dss, bool dst_host, size_t sz, size_t ns,
+                     hipStream_t st) {
+    HostTrace tr;
+    const bool in_bm = sss == sz, out_bm = dss == sz;
+    const size_t per = (src_host ? size_t(k) * sz : 0) + (dst_host ? size_t(r) * sz : 0);
+    size_t gs = std::max<size_t>(1, (size_t(16) << 20) / std::max<size_t>(1, per));
+    if (ns >= 4) gs = std::min(gs, (ns + 3) / 4);  // at least 4 groups, so the stages overlap
+    gs = std::min(gs, ns);
+    const size_t in_bytes = align_up(src_host ? gs * k * sz : 0, 256);
+    const size_t out_bytes = align_up(dst_host ? gs * r * sz : 0, 256);
+    const size_t slot_bytes = in_bytes + out_bytes;
+    if (ensure_sbuf(d, slot_bytes * kStageSlots)) return t_status;
+    uint8_t* const hs = static_cast<uint8_t*>(d.sbuf);
+    uint8_t* const ds = static_cast<uint8_t*>(d.sbuf_dev);
+    HostPool& pool = HostPool::get();
+    CopyLatch lin[kStageSlots], lout[kStageSlots];
+    const size_t ngroups = (ns + gs - 1) / gs;
+    // stripes per copy task when rows are copied one stripe at a time
+    const size_t task_stripes = std::max<size_t>(1, (size_t(1) << 20) / std::max<size_t>(1, per));
+
+    // rows of stripes [s0, s0 + n) between the caller's array (block stride
+    // bs, stripe stride ss) and a slot; `to_slot` picks the direction
+    auto move_rows = [&](uint8_t* slot, gf* user, size_t bs, size_t ss, unsigned nb, bool bm, size_t s0, size_t n,
+                         bool to_slot, CopyLatch* latch) {
+        if (bm) {  // block b of the group: n*sz contiguous bytes on both sides
+            for (unsigned b = 0; b < nb; ++b) {
+                uint8_t* sp = slot + size_t(b) * n * sz;
+                uint8_t* up = user + b * bs + s0 * sz;
+                if (to_slot)
+                    pool.copy_async(sp, up, n * sz, latch);
+                else
+                    pool.copy_async(up, sp, n * sz, latch);
+            }
+            return;
+        }
+        for (size_t t0 = 0; t0 < n; t0 += task_stripes) {
+            const size_t t1 = std::min(n, t0 + task_stripes);
+            pool.run_async(
+                [=]() {
+                    for (size_t s = t0; s < t1; ++s) {
+                        uint8_t* sp = slot + s * nb * sz;
+                        uint8_t* up = user + (s0 + s) * ss;
+                        if (bs == sz) {  // the stripe's rows are contiguous
+                            if (to_slot)
+                                std::memcpy(sp, up, nb * sz);
+                            else
+                                std::memcpy(up, sp, nb * sz);
+                            continue;
+                        }
+                        for (unsigned b = 0; b < nb; ++b) {
+                            if (to_slot)
+                                std::memcpy(sp + b * sz, up + b * bs, sz);
+                            else
+                                std::memcpy(up + b * bs, sp + b * sz, sz);
+                        }
+                    }
+                },
+                latch);
+        }
+    };
+    auto group = [&](size_t g, size_t* s0, size_t* n) {
+        *s0 = g * gs;
+        *n = std::min(gs, ns - *s0);
+    };
+    auto stage_in = [&](size_t g) {
+        if (!src_host) return;
+        size_t s0, n;
+        group(g, &s0, &n);
+        const int s = static_cast<int>(g % kStageSlots);
+        move_rows(hs + s * slot_bytes, const_cast<gf*>(src), sbs, sss, k, in_bm, s0, n, true, &lin[s]);
+    };
+    auto copy_out = [&](size_t g) {
+        if (!dst_host) return;
+        size_t s0, n;
+        group(g, &s0, &n);
+        const int s = static_cast<int>(g % kStageSlots);
+        move_rows(hs + s * slot_bytes + in_bytes, dst, dbs, dss, r, out_bm, s0, n, false, &lout[s]);
+    };
+    auto drain = [&](int status) {
+        (void)hipStreamSynchronize(st);
+        for (int s = 0; s < kStageSlots; ++s) {
+            pool.wait(&lin[s]);
+            pool.wait(&lout[s]);
+        }
+        return status;
+    };
+    std::vector<const uint8_t*> zin(k);
+    std::vector<uint8_t*> zout(r);
+    hipError_t e;
+    tr.mark("classify");
+    stage_in(0);
+    for (size_t g = 0; g < ngroups; ++g) {
+        const int s = static_cast<int>(g % kStageSlots);
+        size_t s0, n;
+        group(g, &s0, &n);
+        pool.wait(&lin[s]);
+        pool.wait(&lout[s]);
+        size_t iss = sss, oss = dss;
+        for (unsigned j = 0; j < k; ++j) zin[j] = src + j * sbs + s0 * sss;
+        for (unsigned i = 0; i < r; ++i) zout[i] = dst + i * dbs + s0 * dss;
+        if (src_host) {
+            uint8_t* b = ds + s * slot_bytes;
+            for (unsigned j = 0; j < k; ++j) zin[j] = b + (in_bm ? size_t(j) * n * sz : size_t(j) * sz);
+            iss = in_bm ? sz : size_t(k) * sz;
+        }
+        if (dst_host) {
+            uint8_t* b = ds + s * slot_bytes + in_bytes;
+            for (unsigned i = 0; i < r; ++i) zout[i] = b + (out_bm ? size_t(i) * n * sz : size_t(i) * sz);
+            oss = out_bm ? sz : size_t(r) * sz;
+        }
+        if (apply_matrix(coef, k, r, zin.data(), zout.data(), sz, n, iss, oss, st)) return drain(t_status);
+        if ((e = hipEventRecord(d.ev_stg[s], st)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
+        if (g + 1 < ngroups) stage_in(g + 1);
+        if (g >= 1) {
+            if ((e = hipEventSynchronize(d.ev_stg[(g - 1) % kStageSlots])) != hipSuccess)
+                return drain(hip_fail(e, "hipEventSynchronize"));
+            copy_out(g - 1);
+        }
+    }
+    if ((e = hipEventSynchronize(d.ev_stg[(ngroups - 1) % kStageSlots])) != hipSuccess)
+        return drain(hip_fail(e, "hipEventSynchronize"));
+    tr.mark("kernels");
+    copy_out(ngroups - 1);
+    drain(FEC_OK);
+    tr.mark("copy-out");
+    return set_status(FEC_OK);
+}
+
 // Run `coef` (r x k) over in -> out.  Device blocks are used in place; host
 // blocks are staged (small calls: one pinned bounce buffer each way; large
 // calls: the chunked pipeline).  Synchronous unless FEC_FLAG_ASYNC and every
@@ -1288,6 +1427,27 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     const unsigned k = code->k;
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
     if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    // pageable host memory on either side: staged through pinned slots
+    // (synchronous whatever the flags; FEC_FLAG_ROW_PADDING does not apply)
+    if (sz && nstripes && r) {
+        const size_t src_ext = (nstripes - 1) * sss + (k - 1) * sbs + sz;
+        const size_t dst_ext = (nstripes - 1) * dss + (r - 1) * dbs + sz;
+        const int sdev = pointer_device(src), ddev0 = pointer_device(dst);
+        const uint8_t* zs = sdev >= 0 ? src : mapped_block(src, src_ext);
+        const uint8_t* zd = ddev0 >= 0 ? dst : mapped_block(dst, dst_ext);
+        if (!zs || !zd) {
+            if (sdev >= 0 && ddev0 >= 0 && sdev != ddev0)
+                return set_status(FEC_EINVAL, "batched entry points take memory on one device");
+            int dev = sdev >= 0 ? sdev : ddev0;
+            if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return set_status(FEC_ENODEV, "no current HIP device");
+            DeviceGuard guard(dev);
+            DevCtx* d = nullptr;
+            if (dev_ctx(dev, &d)) return t_status;
+            hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
+            return run_batch_staged(*d, coef, k, r, zs ? zs : src, sbs, sss, !zs, zd ? const_cast<gf*>(zd) : dst, dbs,
+                                    dss, !zd, sz, nstripes, st);
+        }
+    }
     // Block-major batches (stripes packed back to back inside each block array,
     // both strides == sz) are one stripe of nstripes * sz bytes: output byte x
     // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so

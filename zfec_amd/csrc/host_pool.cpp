@@ -76,7 +76,7 @@ void HostPool::copy_async(void* dst, const void* src, size_t len, CopyLatch* lat
         for (size_t i = 0; i < n; ++i) {
             const size_t off = i * piece;
             queue_.push_back({static_cast<char*>(dst) + off, static_cast<const char*>(src) + off,
-                              std::min(piece, len - off), latch});
+                              std::min(piece, len - off), latch, nullptr});
         }
         latch->pending += n;
     }
@@ -86,13 +86,25 @@ void HostPool::copy_async(void* dst, const void* src, size_t len, CopyLatch* lat
         work_cv_.notify_all();
 }
 
+void HostPool::run_async(std::function<void()> fn, CopyLatch* latch) {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        queue_.push_back({nullptr, nullptr, 0, latch, std::move(fn)});
+        latch->pending += 1;
+    }
+    work_cv_.notify_one();
+}
+
 // Pops one piece and runs it with the lock released; false if the queue is empty.
 bool HostPool::run_one(std::unique_lock<std::mutex>& lk) {
     if (queue_.empty()) return false;
-    const CopyPiece p = queue_.front();
+    CopyPiece p = std::move(queue_.front());
     queue_.pop_front();
     lk.unlock();
-    std::memcpy(p.dst, p.src, p.len);
+    if (p.fn)
+        p.fn();
+    else
+        std::memcpy(p.dst, p.src, p.len);
     lk.lock();
     if (--p.latch->pending == 0) done_cv_.notify_all();
     return true;

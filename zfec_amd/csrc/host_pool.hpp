@@ -13,6 +13,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -29,6 +30,7 @@ struct CopyPiece {
     const void* src;
     size_t len;
     CopyLatch* latch;
+    std::function<void()> fn;  // a task instead of a memcpy when set
 };
 
 class HostPool {
@@ -43,6 +45,9 @@ public:
     // Queue memcpy(dst, src, len) cut into pieces of about `piece` bytes;
     // the latch counts them.  Returns immediately.
     void copy_async(void* dst, const void* src, size_t len, CopyLatch* latch, size_t piece = size_t(1) << 20);
+
+    // Queue a task (e.g. a group of row copies); the latch counts it.
+    void run_async(std::function<void()> fn, CopyLatch* latch);
 
     // Wait for every piece counted by `latch`; the calling thread runs queued
     // pieces (of any latch) while it waits.
