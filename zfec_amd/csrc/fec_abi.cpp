@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <sys/mman.h>
 #include <thread>
@@ -57,6 +58,19 @@ int set_status(int st, const char* fmt = nullptr, ...) {
 
 int hip_fail(hipError_t e, const char* what) {
     return set_status(FEC_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+// No C++ exception crosses the C-ABI: a failed allocation (or a thread the
+// system cannot create) inside a call becomes its status.
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_status(FEC_ENOMEM, "out of host memory");
+    } catch (const std::exception& x) {
+        return set_status(FEC_ENOMEM, "host resources exhausted: %s", x.what());
+    }
 }
 
 unsigned long magic_of(const fec_t* p) {
@@ -853,6 +867,7 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     std::vector<const uint8_t*> zin(k);
     std::vector<uint8_t*> zout(r);
     hipError_t e;
+    try {  // a failed allocation while queueing copies: drain what was queued
     stage_in(0);
     for (size_t c = 0; c < nchunks; ++c) {
         const int s = static_cast<int>(c % kStageSlots);
@@ -888,6 +903,9 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     tr.mark("kernels");
     tr.sums("wait-in", "wait-out", "wait-kernel");
     copy_out(nchunks - 1);
+    } catch (const std::exception& x) {
+        return drain(set_status(FEC_ENOMEM, "staged host path: %s", x.what()));
+    }
     drain(FEC_OK);
     tr.mark("copy-out");
     return set_status(FEC_OK);
@@ -994,6 +1012,7 @@ int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, con
     std::vector<uint8_t*> zout(r);
     hipError_t e;
     tr.mark("classify");
+    try {  // a failed allocation while queueing copies: drain what was queued
     stage_in(0);
     for (size_t g = 0; g < ngroups; ++g) {
         const int s = static_cast<int>(g % kStageSlots);
@@ -1027,6 +1046,9 @@ int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, con
         return drain(hip_fail(e, "hipEventSynchronize"));
     tr.mark("kernels");
     copy_out(ngroups - 1);
+    } catch (const std::exception& x) {
+        return drain(set_status(FEC_ENOMEM, "staged batch path: %s", x.what()));
+    }
     drain(FEC_OK);
     tr.mark("copy-out");
     return set_status(FEC_OK);
@@ -1261,9 +1283,11 @@ FEC_API int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fe
     if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
     if (num_block_nums == 0) return set_status(FEC_OK);
     if (!src || !fecs) return set_status(FEC_EINVAL, "NULL block array");
-    std::vector<uint8_t> rows;
-    encode_rows(code, block_nums, num_block_nums, rows);
-    return run_single(rows.data(), code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
+    return guarded([&] {
+        std::vector<uint8_t> rows;
+        encode_rows(code, block_nums, num_block_nums, rows);
+        return run_single(rows.data(), code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
+    });
 }
 
 namespace {
@@ -1302,7 +1326,7 @@ FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const*
     if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0) return set_status(FEC_OK);
     if (!inpkts || !outpkts) return set_status(FEC_EINVAL, "NULL block array");
-    return run_single(rows.data(), code->k, r, inpkts, outpkts, sz, stream, flags);
+    return guarded([&] { return run_single(rows.data(), code->k, r, inpkts, outpkts, sz, stream, flags); });
 }
 
 FEC_API void fec_decode(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
@@ -1521,10 +1545,12 @@ FEC_API int fec_encode_batch(const fec_t* code, const gf* src, size_t src_block_
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
     if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
     if (num_block_nums == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
-    std::vector<uint8_t> rows;
-    encode_rows(code, block_nums, num_block_nums, rows);
-    return run_batch(code, rows.data(), static_cast<unsigned>(num_block_nums), src, src_block_stride,
-                     src_stripe_stride, dst, dst_block_stride, dst_stripe_stride, sz, nstripes, stream, flags);
+    return guarded([&] {
+        std::vector<uint8_t> rows;
+        encode_rows(code, block_nums, num_block_nums, rows);
+        return run_batch(code, rows.data(), static_cast<unsigned>(num_block_nums), src, src_block_stride,
+                         src_stripe_stride, dst, dst_block_stride, dst_stripe_stride, sz, nstripes, stream, flags);
+    });
 }
 
 FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_stride, size_t src_stripe_stride,
@@ -1535,6 +1561,8 @@ FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_
     unsigned r = 0;
     if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
-    return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
-                     dst_stripe_stride, sz, nstripes, stream, flags);
+    return guarded([&] {
+        return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
+                         dst_stripe_stride, sz, nstripes, stream, flags);
+    });
 }

@@ -72,13 +72,15 @@ void HostPool::copy_async(void* dst, const void* src, size_t len, CopyLatch* lat
     piece = std::max<size_t>(piece, 64u << 10);
     const size_t n = (len + piece - 1) / piece;
     {
+        // counted one by one, so a failed push (bad_alloc) leaves the latch
+        // counting exactly the pieces that will run
         std::lock_guard<std::mutex> g(mu_);
         for (size_t i = 0; i < n; ++i) {
             const size_t off = i * piece;
             queue_.push_back({static_cast<char*>(dst) + off, static_cast<const char*>(src) + off,
                               std::min(piece, len - off), latch, nullptr});
+            latch->pending += 1;
         }
-        latch->pending += n;
     }
     if (n == 1)
         work_cv_.notify_one();
