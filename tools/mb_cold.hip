@@ -315,8 +315,42 @@ int sweep() {
     return 0;
 }
 
+// Row-stride sweep of the production kernel on 256 object-major 1 MiB stripes
+// (rows of sz = 349,526 bytes at stride ld): does the HBM fraction depend on
+// where the 10 rows of a stripe fall relative to each other?
+int ldsweep() {
+    const uint32_t ns = 256;
+    const uint64_t sz = (1u << 20) / 3 + 1;
+    const uint64_t lds[] = {349696, 349696 + 128, 349696 + 512, 349696 + 2048, 352256, 352256 + 4096,
+                            356352 + 8192, 393216, 1u << 19, (1u << 19) + 4096};
+    for (int rnd = 0; rnd < 2; ++rnd)
+        for (uint64_t ld : lds) {
+            const uint64_t fp = uint64_t(K + R) * ld * ns;
+            const int nsets = std::max<int>(2, int((1536ull << 20) / fp) + 1);
+            std::vector<Lay> sets(nsets);
+            for (auto& L : sets) {
+                CK(hipMalloc(&L.in, ns * K * ld));
+                CK(hipMalloc(&L.out, ns * R * ld));
+                CK(hipMemset(L.in, 0x5A, ns * K * ld));
+                L.ld = ld;
+            }
+            CK(hipDeviceSynchronize());
+            const float ms = run_prod(sets, 20, sz, ns);
+            const double bytes = double(K + R) * sz * ns;
+            printf("ldsweep ld=%8llu (ld %% 4096 = %4llu)  %8.1f us  %7.1f GB/s  (%.3f of 8 TB/s)  sets=%d\n",
+                   (unsigned long long)ld, (unsigned long long)(ld % 4096), ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+                   bytes / (ms * 1e-3) / 8e12, nsets);
+            for (auto& L : sets) {
+                CK(hipFree(L.in));
+                CK(hipFree(L.out));
+            }
+        }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
+    if (argc > 1 && std::string(argv[1]) == "ldsweep") return ldsweep();
     if (argc > 1 && std::string(argv[1]) == "walks") return walks();
     const uint32_t ns = argc > 2 ? atoi(argv[2]) : 256;
     const uint64_t sz = (1u << 20) / 3 + 1;  // 349,526
