@@ -111,6 +111,45 @@ __global__ __launch_bounds__(256) void mb(const Lay L) {
     }
 }
 
+// Encode-shaped copy walk (`lane`) whose last workgroups store with a
+// write-through policy (SP: 1 sc1, 2 sc0 sc1, 3 nt sc1) and the rest with nt:
+// does the end-of-kernel write-back of dirty L2 lines set part of the fixed
+// per-launch cost?  Workgroups >= tail_wg take the write-through stores.
+template <int SP>
+__global__ __launch_bounds__(256) void mb_tail(const Lay L, uint32_t tail_wg) {
+    const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= L.units) return;
+    const uint32_t s = u / L.cps, c = u - s * L.cps;
+    const uint64_t ib = uint64_t(s) * K * L.ld + uint64_t(c) * 16;
+    const uint64_t ob = uint64_t(s) * R * L.ld + uint64_t(c) * 16;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < K; ++j) acc ^= *reinterpret_cast<const u32x4*>(L.in + ib + j * L.ld);
+    const bool wt = blockIdx.x >= tail_wg;
+    for (int r = 0; r < R; ++r) {
+        uint8_t* q = L.out + ob + r * L.ld;
+        if (wt)
+            store16_pol<true, SP>(q, acc ^ uint32_t(r));
+        else
+            __builtin_nontemporal_store(acc ^ uint32_t(r), reinterpret_cast<u32x4*>(q));
+    }
+}
+
+template <int SP>
+float run_tail(const std::vector<Lay>& sets, int reps, uint32_t grid, uint32_t tail_wg) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(mb_tail<SP>, dim3(grid), dim3(256), 0, 0, sets[i % sets.size()], tail_wg);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(mb_tail<SP>, dim3(grid), dim3(256), 0, 0, sets[(i + 3) % sets.size()], tail_wg);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
 template <int WALK, bool NTL, bool NTS, int MODE>
 float run(const std::vector<Lay>& sets, int reps, uint32_t grid) {
     hipEvent_t a, b;
@@ -348,8 +387,49 @@ int ldsweep() {
     return 0;
 }
 
+// cfg2's shape (one 64 MiB K=3/M=10 stripe: 3 + 7 rows of 22,369,792 bytes),
+// cold rotation: the nt copy walk with its last fraction f of workgroups
+// storing write-through, against the production kernel.
+int tail() {
+    const uint64_t sz = (64ull << 20) / 3 + 1, ld = (sz + 255) / 256 * 256;
+    const int nsets = int((1536ull << 20) / (10 * ld)) + 1;
+    std::vector<Lay> sets(nsets);
+    for (auto& L : sets) {
+        CK(hipMalloc(&L.in, K * ld));
+        CK(hipMalloc(&L.out, R * ld));
+        CK(hipMemset(L.in, 0x5A, K * ld));
+        CK(hipMemset(L.out, 0, R * ld));
+        L.ld = ld;
+        L.cps = static_cast<uint32_t>(ld / 16);
+        L.units = L.cps;
+    }
+    CK(hipDeviceSynchronize());
+    const uint32_t grid = (sets[0].units + 255) / 256;
+    const double bytes = double(K + R) * ld;
+    auto rep = [&](const char* name, float ms) {
+        printf("tail %-24s %7.2f us  %7.1f GB/s  (%.3f of 8 TB/s)  sets=%d\n", name, ms * 1e3,
+               bytes / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 8e12, nsets);
+    };
+    for (int rnd = 0; rnd < 3; ++rnd) {
+        printf("-- round %d\n", rnd);
+        rep("prod", run_prod(sets, 40, sz, 1));
+        for (double f : {0.0, 0.02, 0.05, 0.1, 0.2, 1.0}) {
+            const uint32_t tw = grid - static_cast<uint32_t>(f * grid);
+            char nm[64];
+            snprintf(nm, sizeof nm, "f=%.2f sc0sc1", f);
+            rep(nm, run_tail<2>(sets, 40, grid, tw));
+            snprintf(nm, sizeof nm, "f=%.2f ntsc1", f);
+            rep(nm, run_tail<3>(sets, 40, grid, tw));
+            snprintf(nm, sizeof nm, "f=%.2f sc1", f);
+            rep(nm, run_tail<1>(sets, 40, grid, tw));
+        }
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
+    if (argc > 1 && std::string(argv[1]) == "tail") return tail();
     if (argc > 1 && std::string(argv[1]) == "ldsweep") return ldsweep();
     if (argc > 1 && std::string(argv[1]) == "walks") return walks();
     const uint32_t ns = argc > 2 ? atoi(argv[2]) : 256;

@@ -1058,6 +1058,7 @@ struct Variant {
     int chunk = kChunk;      // bytes per unit (a lane's slice of one block)
     int pad_tile = 0;        // kTilesPadded: rows per tile (the LDS table is padded to whole tiles)
     bool rows = false;       // matapply_rows: one wave per stripe
+    KernelFn fn_wt = nullptr; // the same kernel with nt sc1 output stores (store_policy)
 };
 
 // Register-table variants: k <= 4, r <= 8.
@@ -1086,6 +1087,26 @@ std::once_flag g_dispatch_once;
 int g_num_cu = 0;
 int g_grid_mult = 1024;  // grid cap = CUs x resident blocks per CU x g_grid_mult (1024: ~one unit per lane; measured +9 % on 10^6 4 KiB stripes vs 16)
 
+// Output store policy of the register kernels (ZFEC_HIP_STORE): "nt" streams
+// every store through the L2 write-back (nt); "ntsc1" writes through the L2
+// at device scope (nt sc1); "auto" (default) takes nt sc1 for single-stripe
+// launches -- a few long rows, where it measured faster: the cfg2 64 MiB
+// K=3/M=10 stripe, encode 68.5 -> 69.1-69.9 % of HBM from cold caches,
+// secondary decode 65.6 -> 68.0 %, bench value +1.2-1.5 % -- and nt for
+// batches of many stripes, where nt sc1 measured slower (256 x 1 MiB
+// object-major 69.5 -> 67.7 %, 10^6 x 4 KiB -1 %; tools/ab_store.sh,
+// profiles/r02_store_ab.log; copy-walk probe: tools/mb_cold.exe tail).
+enum StorePolicy { kStoreNt = 0, kStoreNtSc1 = 1, kStoreAuto = 2 };
+StorePolicy store_policy() {
+    static const StorePolicy p = [] {
+        const char* e = getenv("ZFEC_HIP_STORE");
+        if (e && !strcmp(e, "nt")) return kStoreNt;
+        if (e && !strcmp(e, "ntsc1")) return kStoreNtSc1;
+        return kStoreAuto;
+    }();
+    return p;
+}
+
 template <int K, int R>
 void set_reg() {
     // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
@@ -1096,6 +1117,7 @@ void set_reg() {
     // variant "PF AL"; the 3-row decode is unchanged either way)
     constexpr bool kArgLoad = K * R * 5 >= 50;
     g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch, 0, kArgLoad>, kRegNames[K][R], 0, true};
+    g_reg[K][R].fn_wt = matapply_reg<K, R, true, 1, 3, kPrefetch, 0, kArgLoad>;
     snprintf(g_rows_names[K][R], sizeof g_rows_names[K][R], "matapply_rows<%d,%d>", K, R);
     g_rows[K][R] = Variant{matapply_rows<K, R, kArgLoad>, g_rows_names[K][R], 0, true};
     g_rows[K][R].rows = true;
@@ -1339,7 +1361,10 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     // tools/mb_cold.hip, profiles/r02_mb_cold.log)
     const char* xe = getenv("ZFEC_HIP_XCD");
     job.xcd_swizzle = (xe && xe[0] == '1') && !v->rows;
-    hipLaunchKernelGGL(v->fn, dim3(grid), dim3(kBlock), lds, stream, job);
+    KernelFn fn = v->fn;
+    if (v->fn_wt && (store_policy() == kStoreNtSc1 || (store_policy() == kStoreAuto && job.nstripes == 1)))
+        fn = v->fn_wt;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, stream, job);
     t_last_kernel = v->name;
     return hipGetLastError();
 }
