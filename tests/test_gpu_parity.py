@@ -516,6 +516,10 @@ _LAYOUTS = {
                        out_bs=3 * 1024 * 1024 + 128, out_ss=0, seed=13, guard=96),
     "object_major": dict(k=4, m=9, sz=5000, ns=700, in_bs=5000, in_ss=4 * 5000, out_bs=5000, out_ss=5 * 5000,
                          seed=14, guard=96),
+    # one long K=3/M=10 stripe on the register kernel (nt sc1 stores by default
+    # on single-stripe launches), output rows at an odd stride
+    "one_stripe_reg": dict(k=3, m=10, sz=5 * 1024 * 1024 + 13, ns=1, in_bs=5 * 1024 * 1024 + 64, in_ss=0,
+                           out_bs=5 * 1024 * 1024 + 40, out_ss=0, seed=15, guard=96),
 }
 
 
@@ -537,12 +541,13 @@ def _run_child(spec, env_extra, tmp_path, tag):
 
 @pytest.mark.parametrize("layout", sorted(_LAYOUTS))
 def test_batch_layout_env_variants(layout, tmp_path):
-    """The same fec_encode_batch run three ways, each in its own process since
+    """The same fec_encode_batch run five ways, each in its own process since
     the knobs are read once: as shipped, with the block-major collapse off
-    (ZFEC_HIP_BATCH_COLLAPSE=0), and with at most 1024 units per launch
+    (ZFEC_HIP_BATCH_COLLAPSE=0), with at most 1024 units per launch
     (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte ranges, batches
-    into stripe groups).  All three outputs, guard bytes included, must be
-    identical, and sampled stripes must equal the oracle's parity."""
+    into stripe groups), and with the register kernels' store policy forced
+    to nt and to nt sc1 (ZFEC_HIP_STORE).  All outputs, guard bytes included,
+    must be identical, and sampled stripes must equal the oracle's parity."""
     import importlib.util
     import os
 
@@ -552,6 +557,9 @@ def test_batch_layout_env_variants(layout, tmp_path):
     split, _ = _run_child(spec, {"ZFEC_HIP_LAUNCH_UNITS": "1024"}, tmp_path, "split")
     assert np.array_equal(base, nocol), "collapse changed the output"
     assert np.array_equal(base, split), "launch splitting changed the output"
+    for pol in ("nt", "ntsc1"):
+        got, _ = _run_child(spec, {"ZFEC_HIP_STORE": pol}, tmp_path, "store_" + pol)
+        assert np.array_equal(base, got), "store policy %s changed the output" % pol
     child = importlib.util.spec_from_file_location(
         "gpu_batch_child", os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpu_batch_child.py"))
     mod = importlib.util.module_from_spec(child)
