@@ -50,6 +50,21 @@ from zfec_amd import capi  # noqa: E402
 from zfec_amd.shard import shard_range, slab_range  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# Cold-cache HBM rates of loads alone and of stores alone in this library's access pattern
+# (tools/mb_cold.exe read3 / write7, best of the runs in profiles/r02_mb_cold.log).  HBM does
+# not overlap this pattern's reads with its writes (a cold encode takes read3 + write7), so a
+# launch reading R and writing W bytes needs at least R / READ + W / WRITE.
+HBM_READ_GBPS, HBM_WRITE_GBPS = 6449.0, 5799.0
+
+
+def rw_ceiling(read_bytes, write_bytes, achieved_gbps):
+    """The read-then-write ceiling of one launch's traffic and the achieved fraction of it."""
+    c = (read_bytes + write_bytes) / (read_bytes / HBM_READ_GBPS + write_bytes / HBM_WRITE_GBPS)
+    return {"GBps": round(c, 1), "frac_of_peak": round(c / HBM_PEAK_GBPS, 4),
+            "achieved_frac_of_ceiling": round(achieved_gbps / c, 4),
+            "basis": "(R + W) / (R / %.0f + W / %.0f GB/s): cold loads-only and stores-only rates of the same "
+                     "walk (tools/mb_cold.exe read3 / write7, profiles/r02_mb_cold.log)" % (HBM_READ_GBPS,
+                                                                                        HBM_WRITE_GBPS)}
 METRIC = "encode+decode GB/s (device-resident input) at K/M; % of HBM roofline"
 
 # name: (k, m, stripe bytes, stripes, scaling)
@@ -810,6 +825,7 @@ def main():
                      "frac_warm": round(gbps(enc_bytes, t["enc_ms_warm"]) / HBM_PEAK_GBPS, 4),
                      "launch_ms_warm": round(t["enc_ms_warm"], 4),
                      "launch_ms_event_pairs": round(t["enc_ms_pairs"], 4),
+                     "rw_ceiling": rw_ceiling(k * sz * ns, r * sz * ns, gbps(enc_bytes, t["enc_ms"])),
                      "host_enqueue_us": round(t["enqueue_us"][0], 1),
                      "timing": timing},
         "decode_roofline": {"achieved": round(gbps(dec_bytes, t["dec_ms"]), 1),
@@ -818,7 +834,8 @@ def main():
                             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(t["dec_ms"], 4),
                             "frac_warm": round(gbps(dec_bytes, t["dec_ms_warm"]) / HBM_PEAK_GBPS, 4),
                             "launch_ms_warm": round(t["dec_ms_warm"], 4),
-                            "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4)},
+                            "launch_ms_event_pairs": round(t["dec_ms_pairs"], 4),
+                            "rw_ceiling": rw_ceiling(k * sz * ns, nrec * sz * ns, gbps(dec_bytes, t["dec_ms"]))},
         "valu_roofline": None if args.slabs else valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
         "streams": args.streams,
