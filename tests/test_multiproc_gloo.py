@@ -188,3 +188,17 @@ def test_node_barrier_shared_memory(world):
     assert sorted(r for r, _, _ in res) == list(range(world))
     assert all(ok and epoch == 200 for _, ok, epoch in res)
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("zfec_bench_barrier_")]
+
+
+def test_rw_ceiling_bounds():
+    """bench.py's read-then-write ceiling: between the stores-only and the
+    loads-only rate, equal to each at the extremes, and the achieved fraction
+    is the achieved rate over it."""
+    import bench
+
+    c = bench.rw_ceiling(3, 7, 5000.0)
+    assert bench.HBM_WRITE_GBPS < c["GBps"] < bench.HBM_READ_GBPS
+    assert abs(bench.rw_ceiling(1, 0, 1.0)["GBps"] - bench.HBM_READ_GBPS) < 0.1
+    assert abs(bench.rw_ceiling(0, 1, 1.0)["GBps"] - bench.HBM_WRITE_GBPS) < 0.1
+    assert abs(c["achieved_frac_of_ceiling"] - 5000.0 / c["GBps"]) < 1e-3
+    assert abs(c["frac_of_peak"] - c["GBps"] / bench.HBM_PEAK_GBPS) < 1e-3
