@@ -427,8 +427,36 @@ int tail() {
     return 0;
 }
 
+// Fixed cost of a launch: back-to-back launches of a kernel that does no
+// memory work, with one workgroup and with the cfg2 encode's grid (one
+// 16-byte unit per lane of a 22,369,792-byte row: 5,462 workgroups of 256).
+__global__ __launch_bounds__(256) void mb_empty(uint32_t* out, uint32_t v) {
+    if (v == 0x12345678u && threadIdx.x == 0) out[blockIdx.x] = v;
+}
+
+int launch_cost() {
+    uint32_t* out;
+    CK(hipMalloc(&out, 1 << 20));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (uint32_t grid : {1u, 256u, 5462u, 21845u, 87381u}) {
+        for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(mb_empty, dim3(grid), dim3(256), 0, 0, out, 1u);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a, 0));
+        for (int i = 0; i < 200; ++i) hipLaunchKernelGGL(mb_empty, dim3(grid), dim3(256), 0, 0, out, 1u);
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        printf("launch grid=%6u x 256  %6.2f us per launch (back to back, empty kernel)\n", grid, ms * 1e3 / 200);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
+    if (argc > 1 && std::string(argv[1]) == "launch") return launch_cost();
     if (argc > 1 && std::string(argv[1]) == "tail") return tail();
     if (argc > 1 && std::string(argv[1]) == "ldsweep") return ldsweep();
     if (argc > 1 && std::string(argv[1]) == "walks") return walks();
