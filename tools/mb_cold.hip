@@ -427,6 +427,64 @@ int tail() {
     return 0;
 }
 
+// The `lane` copy walk with BS-thread workgroups (256 in production): fewer,
+// larger workgroups cost less to dispatch (launch_cost) -- does the walk gain?
+template <int BS>
+__global__ __launch_bounds__(BS) void mb_bs(const Lay L) {
+    const uint32_t u = blockIdx.x * BS + threadIdx.x;
+    if (u < L.units) unit_io(L, u, false, true, 0);
+}
+
+template <int BS>
+float run_bs(const std::vector<Lay>& sets, int reps) {
+    const uint32_t grid = (sets[0].units + BS - 1) / BS;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(mb_bs<BS>, dim3(grid), dim3(BS), 0, 0, sets[i % sets.size()]);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(mb_bs<BS>, dim3(grid), dim3(BS), 0, 0, sets[(i + 3) % sets.size()]);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+// 256 object-major 1 MiB stripes (as main) and the cfg2 stripe, cold: the
+// copy walk at 256 / 512 / 1024 threads per workgroup.
+int blocks() {
+    for (int shape = 0; shape < 2; ++shape) {
+        const uint32_t ns = shape == 0 ? 256 : 1;
+        const uint64_t sz = shape == 0 ? (1u << 20) / 3 + 1 : (64ull << 20) / 3 + 1;
+        const uint64_t ld = (sz + 255) / 256 * 256;
+        const int nsets = std::max<int>(2, int((1536ull << 20) / (10 * ld * ns)) + 1);
+        std::vector<Lay> sets(nsets);
+        for (auto& L : sets) {
+            CK(hipMalloc(&L.in, ns * K * ld));
+            CK(hipMalloc(&L.out, ns * R * ld));
+            CK(hipMemset(L.in, 0x5A, ns * K * ld));
+            L.ld = ld;
+            L.cps = static_cast<uint32_t>(ld / 16);
+            L.units = L.cps * ns;
+        }
+        CK(hipDeviceSynchronize());
+        const double bytes = double(K + R) * ld * ns;
+        for (int rnd = 0; rnd < 3; ++rnd) {
+            const float t256 = run_bs<256>(sets, 20), t512 = run_bs<512>(sets, 20), t1024 = run_bs<1024>(sets, 20);
+            printf("blocks %s  256: %7.2f us (%.3f)  512: %7.2f us (%.3f)  1024: %7.2f us (%.3f)\n",
+                   shape == 0 ? "256 x 1 MiB object-major" : "cfg2 64 MiB stripe      ", t256 * 1e3,
+                   bytes / (t256 * 1e-3) / 8e12, t512 * 1e3, bytes / (t512 * 1e-3) / 8e12, t1024 * 1e3,
+                   bytes / (t1024 * 1e-3) / 8e12);
+        }
+        for (auto& L : sets) {
+            CK(hipFree(L.in));
+            CK(hipFree(L.out));
+        }
+    }
+    return 0;
+}
+
 // Fixed cost of a launch: back-to-back launches of a kernel that does no
 // memory work, with one workgroup and with the cfg2 encode's grid (one
 // 16-byte unit per lane of a 22,369,792-byte row: 5,462 workgroups of 256).
@@ -457,6 +515,7 @@ int launch_cost() {
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
     if (argc > 1 && std::string(argv[1]) == "launch") return launch_cost();
+    if (argc > 1 && std::string(argv[1]) == "blocks") return blocks();
     if (argc > 1 && std::string(argv[1]) == "tail") return tail();
     if (argc > 1 && std::string(argv[1]) == "ldsweep") return ldsweep();
     if (argc > 1 && std::string(argv[1]) == "walks") return walks();
