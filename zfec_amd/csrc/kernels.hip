@@ -376,7 +376,7 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
 // ---------------------------------------------------------------------------
 constexpr uint64_t kRowsMin = 1024, kRowsMax = 4096;
 
-template <int K, int R, bool AL>
+template <int K, int R, bool AL, bool PRE = false>
 __global__ __launch_bounds__(kBlock) void matapply_rows(const MatJob job) {
     Tab T[R][K];
     if constexpr (!AL) {
@@ -389,11 +389,30 @@ __global__ __launch_bounds__(kBlock) void matapply_rows(const MatJob job) {
     const uint32_t waves = gridDim.x * (kBlock / 64);
     const uint64_t sz = job.sz;
     for (uint32_t s = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); s < job.nstripes; s += waves) {
-        for (uint64_t off = lane * 16u; off < sz; off += 1024u) {
-            const uint64_t o = off + 16u <= sz ? off : sz - 16u;
-            u32x4 x[K];
-            reg_load<K>(job, x, s * job.in_sstride + o, true, 16u);
-            reg_compute_store<K, R, true, 0, AL>(job, T, x, s * job.out_sstride + o, true, 16u);
+        if constexpr (PRE) {
+            // PRE (default): every piece of the lane's share of the stripe (at
+            // most 4: sz <= 4 KiB) loaded before any is computed, so all of the
+            // wave's loads are in flight at once
+            u32x4 x[4][K];
+            uint64_t o[4];
+            bool live[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint64_t off = lane * 16u + 1024u * h;
+                live[h] = off < sz;
+                o[h] = off + 16u <= sz ? off : sz - 16u;
+                if (live[h]) reg_load<K>(job, x[h], s * job.in_sstride + o[h], true, 16u);
+            }
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                if (live[h]) reg_compute_store<K, R, true, 0, AL>(job, T, x[h], s * job.out_sstride + o[h], true, 16u);
+        } else {
+            for (uint64_t off = lane * 16u; off < sz; off += 1024u) {
+                const uint64_t o = off + 16u <= sz ? off : sz - 16u;
+                u32x4 x[K];
+                reg_load<K>(job, x, s * job.in_sstride + o, true, 16u);
+                reg_compute_store<K, R, true, 0, AL>(job, T, x, s * job.out_sstride + o, true, 16u);
+            }
         }
     }
 }
@@ -1119,7 +1138,16 @@ void set_reg() {
     g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch, 0, kArgLoad>, kRegNames[K][R], 0, true};
     g_reg[K][R].fn_wt = matapply_reg<K, R, true, 1, 3, kPrefetch, 0, kArgLoad>;
     snprintf(g_rows_names[K][R], sizeof g_rows_names[K][R], "matapply_rows<%d,%d>", K, R);
-    g_rows[K][R] = Variant{matapply_rows<K, R, kArgLoad>, g_rows_names[K][R], 0, true};
+    // the row walk loads every piece of a lane's share of the stripe before
+    // computing any (cfg5 encode 67.7 -> 70.1 % of HBM cold, decode 66.7 -> 69.8 %,
+    // tools/ab_store.sh, profiles/r02_rows_pre_ab.log); ZFEC_HIP_ROWS_PRE=0: one
+    // piece at a time (A/B)
+    static const bool rows_pre = [] {
+        const char* e = getenv("ZFEC_HIP_ROWS_PRE");
+        return !(e && e[0] == '0');
+    }();
+    g_rows[K][R] = Variant{rows_pre ? matapply_rows<K, R, kArgLoad, true> : matapply_rows<K, R, kArgLoad>,
+                           g_rows_names[K][R], 0, true};
     g_rows[K][R].rows = true;
 }
 
