@@ -520,6 +520,9 @@ _LAYOUTS = {
     # on single-stripe launches), output rows at an odd stride
     "one_stripe_reg": dict(k=3, m=10, sz=5 * 1024 * 1024 + 13, ns=1, in_bs=5 * 1024 * 1024 + 64, in_ss=0,
                            out_bs=5 * 1024 * 1024 + 40, out_ss=0, seed=15, guard=96),
+    # many short blocks (the row walk, matapply_rows), rows at odd strides
+    "rows_object_major": dict(k=3, m=10, sz=1366, ns=300, in_bs=1400, in_ss=3 * 1400 + 24, out_bs=1390,
+                              out_ss=7 * 1390 + 8, seed=16, guard=96),
 }
 
 
@@ -541,13 +544,14 @@ def _run_child(spec, env_extra, tmp_path, tag):
 
 @pytest.mark.parametrize("layout", sorted(_LAYOUTS))
 def test_batch_layout_env_variants(layout, tmp_path):
-    """The same fec_encode_batch run five ways, each in its own process since
+    """The same fec_encode_batch run six ways, each in its own process since
     the knobs are read once: as shipped, with the block-major collapse off
     (ZFEC_HIP_BATCH_COLLAPSE=0), with at most 1024 units per launch
     (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte ranges, batches
-    into stripe groups), and with the register kernels' store policy forced
-    to nt and to nt sc1 (ZFEC_HIP_STORE).  All outputs, guard bytes included,
-    must be identical, and sampled stripes must equal the oracle's parity."""
+    into stripe groups), with the register kernels' store policy forced to nt
+    and to nt sc1 (ZFEC_HIP_STORE), and with the row walk taking one piece at
+    a time (ZFEC_HIP_ROWS_PRE=0).  All outputs, guard bytes included, must be
+    identical, and sampled stripes must equal the oracle's parity."""
     import importlib.util
     import os
 
@@ -560,6 +564,10 @@ def test_batch_layout_env_variants(layout, tmp_path):
     for pol in ("nt", "ntsc1"):
         got, _ = _run_child(spec, {"ZFEC_HIP_STORE": pol}, tmp_path, "store_" + pol)
         assert np.array_equal(base, got), "store policy %s changed the output" % pol
+    if layout == "rows_object_major":
+        assert "matapply_rows" in kern, kern
+    one, _ = _run_child(spec, {"ZFEC_HIP_ROWS_PRE": "0"}, tmp_path, "rows_one_piece")
+    assert np.array_equal(base, one), "the one-piece row walk changed the output"
     child = importlib.util.spec_from_file_location(
         "gpu_batch_child", os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpu_batch_child.py"))
     mod = importlib.util.module_from_spec(child)
