@@ -98,6 +98,9 @@ struct DevCtx {
     void* sbuf_dev = nullptr;
     size_t scap = 0;
     hipEvent_t ev_stg[kStageSlots] = {};
+    uint32_t* flag = nullptr;      // pinned completion word of small synchronous calls
+    uint32_t* flag_dev = nullptr;  // its address in the device's view
+    uint32_t seq = 0;
 };
 
 struct ThreadCtx {
@@ -122,6 +125,7 @@ struct ThreadCtx {
             if (d.dbuf) (void)hipFree(d.dbuf);
             if (d.hbuf) (void)hipHostFree(d.hbuf);
             if (d.sbuf) (void)hipHostFree(d.sbuf);
+            if (d.flag) (void)hipHostFree(d.flag);
             (void)hipSetDevice(cur);
         }
     }
@@ -217,6 +221,52 @@ int gpu_available() {
         return 0;
     }
     return n;
+}
+
+// Small synchronous calls (one-workgroup register-kernel launches): the
+// kernel publishes completion in pinned host memory and the calling thread
+// spins on it -- launch to return 6.4-6.9 us against 12.2 us through
+// hipStreamSynchronize (tools/mb_sync.hip, profiles/r02_sync_probe.log).
+// The stream is queried every 1024 spins, so an error ends the wait; past
+// 200 us it blocks in hipStreamSynchronize.  ZFEC_HIP_WAIT=sync turns it off.
+uint32_t* signal_slot(DevCtx& d) {
+    static const bool on = [] {
+        const char* e = getenv("ZFEC_HIP_WAIT");
+        return !(e && !strcmp(e, "sync"));
+    }();
+    if (!on) return nullptr;
+    if (!d.flag) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        void* pd = nullptr;
+        if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess || !pd) {
+            (void)hipGetLastError();
+            pd = p;
+        }
+        d.flag = static_cast<uint32_t*>(p);
+        d.flag_dev = static_cast<uint32_t*>(pd);
+        __atomic_store_n(d.flag, 0u, __ATOMIC_RELEASE);
+    }
+    if (++d.seq == 0) d.seq = 1;
+    return d.flag_dev;
+}
+
+hipError_t wait_signal(DevCtx& d, hipStream_t st) {
+    const uint32_t seq = d.seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t n = 1;; ++n) {
+        if (__atomic_load_n(d.flag, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+        if ((n & 1023u) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return hipSuccess;  // the stream is idle: the kernel has finished
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+        }
+    }
+    return hipStreamSynchronize(st);
 }
 
 // RAII: restore the caller's current device.
@@ -1157,11 +1207,19 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // them zero-copy (A/B runs).
     const char* zcw = getenv("ZFEC_HIP_ZC_WIDE");
     const bool zc_kernel = (k <= 4 && r <= 8) || (zcw && zcw[0] == '1');
+    bool signalled = false;
     if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = hbd + slot * (nin + q);
-        if (apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st)) return t_status;
+        // one launch of at most one workgroup (k <= 4, r <= 8, sz <= 4 KiB): it
+        // signals its own completion
+        if (k <= 4 && r <= 8 && sz <= 4096)
+            if (uint32_t* f = signal_slot(*d)) matapply_request_signal(f, d->seq);
+        const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st);
+        signalled = st0 == FEC_OK && matapply_signal_used();
+        matapply_request_signal(nullptr, 0);  // an unconsumed request must not reach a later launch
+        if (st0) return t_status;
     } else {
         if (ensure_dbuf(*d, slot * nhost)) return t_status;
         uint8_t* base = static_cast<uint8_t*>(d->dbuf);
@@ -1174,7 +1232,8 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
                                         st)) != hipSuccess)
             return hip_fail(e, "hipMemcpyAsync D2H");
     }
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    if ((e = signalled ? wait_signal(*d, st) : hipStreamSynchronize(st)) != hipSuccess)
+        return hip_fail(e, "hipStreamSynchronize");
     copy_blocks(false);
     return set_status(FEC_OK);
 }

@@ -341,8 +341,7 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
             ob = v.s * job.out_sstride + spn.off;
             u = v;
         }
-        return;
-    }
+    } else {
     while (u.s < job.nstripes) {
         uint64_t ib[U], ob[U];
         uint32_t nb[U];
@@ -362,6 +361,17 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
 #pragma unroll
         for (int i = 0; i < U; ++i)
             if (live[i]) reg_compute_store<K, R, NT, SP, AL>(job, T, x[i], ob[i], full[i], nb[i]);
+    }
+    }
+    // one-workgroup launches of a synchronous small call: publish completion
+    // in pinned host memory (every wave's stores complete at system scope,
+    // then one lane's flag store), so the host need not wait in
+    // hipStreamSynchronize (fec_abi.cpp run_single)
+    if (job.done_flag) {
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(job.done_flag, job.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1207,6 +1217,9 @@ Variant* pick(uint32_t k, uint32_t r, bool acc, uint64_t sz = 0, uint64_t nstrip
 }
 
 thread_local const char* t_last_kernel = "";
+thread_local uint32_t* t_signal_flag = nullptr;
+thread_local uint32_t t_signal_seq = 0;
+thread_local bool t_signal_used = false;
 
 // ---- matapply_bsg dispatch ------------------------------------------------------
 // Rows per wave: the smallest instantiated RT >= ceil(r / 4).
@@ -1324,7 +1337,18 @@ const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate) {
 
 const char* matapply_last_kernel() { return t_last_kernel; }
 
+void matapply_request_signal(uint32_t* flag_dev, uint32_t seq) {
+    t_signal_flag = flag_dev;
+    t_signal_seq = seq;
+}
+
+bool matapply_signal_used() { return t_signal_used; }
+
 hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
+    uint32_t* const sig = t_signal_flag;  // a request covers this launch only
+    t_signal_flag = nullptr;
+    t_signal_used = false;
+    job.done_flag = nullptr;
     if (job.k == 0 || job.k > static_cast<uint32_t>(kMaxIn) || job.r == 0 || job.r > static_cast<uint32_t>(kMaxOut) ||
         job.r * job.k > static_cast<uint32_t>(kMaxCoef) || job.nstripes == 0 || job.sz == 0)
         return hipErrorInvalidValue;
@@ -1392,6 +1416,11 @@ hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
     KernelFn fn = v->fn;
     if (v->fn_wt && (store_policy() == kStoreNtSc1 || (store_policy() == kStoreAuto && job.nstripes == 1)))
         fn = v->fn_wt;
+    if (sig && v->fn_wt && grid == 1) {  // a register kernel (fn_wt: only they have one), one workgroup
+        job.done_flag = sig;
+        job.done_seq = t_signal_seq;
+        t_signal_used = true;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, stream, job);
     t_last_kernel = v->name;
     return hipGetLastError();

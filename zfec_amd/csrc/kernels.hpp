@@ -35,6 +35,9 @@ struct alignas(16) MatJob {
                            // 2 = coef[] is in matapply_bsg's walk order
     uint32_t xcd_swizzle;  // set by launch_matapply: 1 = workgroups dealt XCD-contiguously (UnitIter)
     uint32_t pad_;
+    uint32_t* done_flag;   // set by launch_matapply: pinned host word the kernel's one workgroup
+    uint32_t done_seq;     //   stores done_seq into when it has finished (matapply_request_signal)
+    uint32_t pad2_;
     const uint8_t* in[kMaxIn];
     uint8_t* out[kMaxOut];
     union {
@@ -49,6 +52,13 @@ constexpr int kMaxKernargTables = kMaxCoef / 4 / 5;  // 76 coefficients
 // compile-time limits before launching (returns hipErrorInvalidValue
 // otherwise); chooses the specialised variant for (k, r) when one exists.
 hipError_t launch_matapply(MatJob& job, hipStream_t stream);
+
+// Ask the calling thread's next launch_matapply to have its kernel publish
+// `seq` at flag_dev (pinned host memory) when it has finished -- honoured
+// only by the register kernels in a one-workgroup launch (a stripe of at
+// most 4 KiB per block); matapply_signal_used() says whether it was.
+void matapply_request_signal(uint32_t* flag_dev, uint32_t seq);
+bool matapply_signal_used();
 
 // Name of the table-kernel variant launch_matapply uses for (k, r) when no
 // run-time specialised kernel applies (for tests / profiling).
