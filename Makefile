@@ -18,13 +18,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC 
 
 all: $(LIB) $(PYEXT) oracle
 
-$(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp $(SRC)/bitslice.hpp
+$(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp $(SRC)/bitslice.hpp $(SRC)/config.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp
+$(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/config.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/host_pool.hpp include/zfec_hip.h
+$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/host_pool.hpp $(SRC)/config.hpp include/zfec_hip.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(SRC)/gf256.o: $(SRC)/gf256.cpp $(SRC)/gf256.hpp
@@ -33,7 +33,10 @@ $(SRC)/gf256.o: $(SRC)/gf256.cpp $(SRC)/gf256.hpp
 $(SRC)/host_pool.o: $(SRC)/host_pool.cpp $(SRC)/host_pool.hpp
 	$(CXX) -O2 -std=c++17 -fPIC -fvisibility=hidden -Wall -c $< -o $@
 
-$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o $(SRC)/host_pool.o
+$(SRC)/config.o: $(SRC)/config.cpp $(SRC)/config.hpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o $(SRC)/host_pool.o $(SRC)/config.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -ldl -lpthread
 
 $(PYEXT): $(SRC)/fecmodule.cpp include/zfec_hip.h $(LIB)
@@ -42,6 +45,40 @@ $(PYEXT): $(SRC)/fecmodule.cpp include/zfec_hip.h $(LIB)
 oracle:
 	$(MAKE) -C oracle liboracle.so
 
+# Host-code sanitizer builds (no GPU needed): every host object of the library
+# compiled with AddressSanitizer / ThreadSanitizer (device code unchanged) and
+# linked into tests/c/sanitize_driver.cpp, which runs the library's host-side
+# concurrency and validation paths; the log goes to profiles/.
+SANSRC   := $(SRC)/kernels.hip $(SRC)/fec_abi.cpp $(SRC)/gf256.cpp $(SRC)/bitslice.cpp $(SRC)/host_pool.cpp \
+            $(SRC)/config.cpp tests/c/sanitize_driver.cpp
+SANFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -fPIC -O1 -g -fno-omit-frame-pointer -std=c++17 -Wall \
+            -Wno-unused-function
+
+build/%/driver: $(SANSRC) $(SRC)/*.hpp include/zfec_hip.h
+	mkdir -p build/$*
+	set -e; for f in $(SANSRC); do \
+	  $(HIPCC) $(SANFLAGS) -Xarch_host -fsanitize=$* -c $$f -o build/$*/$$(basename $$f).o; done
+	$(HIPCC) --offload-arch=$(ARCH) -fsanitize=$* -fno-gpu-sanitize -o $@ build/$*/*.o -ldl -lpthread
+
+asan: build/address/driver
+	ASAN_OPTIONS=detect_leaks=0 ./build/address/driver
+
+tsan: build/thread/driver
+	TSAN_OPTIONS="halt_on_error=0 second_deadlock_stack=1" ./build/thread/driver
+
+# The no-GPU Python tests of the C-ABI (tests/test_cpu_surface.py: validation,
+# JIT registry from threads) against an AddressSanitizer build of the library,
+# loaded through zfec_amd.capi (ZFEC_HIP_LIB) with the ASan runtime preloaded.
+ASANRT := $(shell $(HIPCC) -print-file-name=libclang_rt.asan-x86_64.so 2>/dev/null)
+build/address/libzfec_hip.so: build/address/driver
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fsanitize=address -shared-libasan -fno-gpu-sanitize -o $@ \
+	  $(filter-out build/address/sanitize_driver.cpp.o,$(wildcard build/address/*.o)) -ldl -lpthread
+
+asan-py: build/address/libzfec_hip.so
+	ASAN_OPTIONS=detect_leaks=0 LD_PRELOAD=$(ASANRT) ZFEC_HIP_LIB=$(CURDIR)/build/address/libzfec_hip.so \
+	  $(PY) -m pytest tests/test_cpu_surface.py -q -p no:cacheprovider \
+	  -k "rejects or jit_prepare or fec_new or symbols or decode_matrix or invert_vdm or enc_matrix"
+
 ref:
 	$(MAKE) -C oracle ref
 
@@ -49,4 +86,4 @@ clean:
 	rm -f $(SRC)/*.o $(LIB) $(PYEXT)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle ref clean asan tsan asan-py

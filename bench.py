@@ -147,7 +147,12 @@ class NodeBarrier:
 
     def __init__(self, dist, rank, world):
         self.world, self.rank, self.epoch, self.flags = world, rank, 0, None
-        if dist is None or world == 1 or os.environ.get("ZFEC_BENCH_BARRIER") == "dist":
+        # one node only: every rank must be able to map rank 0's /dev/shm page
+        # (torchrun sets LOCAL_WORLD_SIZE; a multi-node job falls back to
+        # dist.barrier())
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if (dist is None or world == 1 or local_world != world
+                or os.environ.get("ZFEC_BENCH_BARRIER") == "dist"):
             self.dist = dist if world > 1 else None
             return
         import mmap

@@ -97,8 +97,8 @@ enum {
                                       each row ends on a whole cache line; output bytes past sz are
                                       then unspecified.  Used only when the block and stripe strides
                                       leave that much room; otherwise ignored */
-#define FEC_FLAG_NO_POPULATE 32u   /* large pageable host outputs: do not pre-fault them from several
-                                      threads before page-locking them (A/B runs; results identical) */
+#define FEC_FLAG_NO_POPULATE 32u   /* accepted and ignored (round 2's page-locking host path, which
+                                      pre-faulted outputs, was removed: the staged path never locks) */
 
 /* Status of the last library call made by this thread, and its message. */
 int fec_last_status(void);
@@ -113,8 +113,10 @@ const char* fec_last_error_message(void);
  *
  * Host buffers: page-locked ones (fec_host_alloc, hipHostMalloc,
  * hipHostRegister) are read and written by the kernel in place over PCIe;
- * large pageable ones are page-locked for the duration of the call and then
- * treated the same way; small pageable ones go through a bounce buffer. */
+ * large pageable ones are copied through pinned staging slots by the
+ * library's host threads, chunk by chunk, overlapped with the kernels; small
+ * pageable ones go through a bounce buffer.  Calls with pageable host buffers
+ * are synchronous whatever the flags. */
 int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fecs,
                   const unsigned* block_nums, size_t num_block_nums, size_t sz,
                   void* stream, unsigned flags);
@@ -147,6 +149,30 @@ int fec_decode_batch(const fec_t* code,
                      gf* dst, size_t dst_block_stride, size_t dst_stripe_stride,
                      const unsigned* index, size_t sz, size_t nstripes,
                      void* stream, unsigned flags);
+
+/* Batched calls over several GPUs of this process.  The nstripes stripes are
+ * split into contiguous, balanced ranges, one per entry of devices[] (entry d
+ * gets stripes [d*q + min(d, e), ...), q = nstripes / ndevices, e = the
+ * remainder: zfec_amd.shard.shard_range), and every range runs on its device
+ * from a persistent host thread of the library bound to that device, with its
+ * own stream and pinned staging slots; the call returns when all are done.
+ * src / dst must be host memory (pageable: staged per device; page-locked:
+ * read and written in place), each GPU moving its share over its own PCIe
+ * link.  A device may be listed more than once (several threads on one GPU).
+ * Layout, block numbers and flags as fec_encode_batch / fec_decode_batch
+ * (FEC_FLAG_ASYNC and FEC_FLAG_LIBRARY_STREAM do not apply: the call is
+ * synchronous on the library's streams).  The first failing range's status
+ * is returned, its message prefixed with the device. */
+int fec_encode_batch_multi(const fec_t* code,
+                           const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                           gf* dst, size_t dst_block_stride, size_t dst_stripe_stride,
+                           const unsigned* block_nums, size_t num_block_nums, size_t sz, size_t nstripes,
+                           const int* devices, size_t ndevices, unsigned flags);
+int fec_decode_batch_multi(const fec_t* code,
+                           const gf* src, size_t src_block_stride, size_t src_stripe_stride,
+                           gf* dst, size_t dst_block_stride, size_t dst_stripe_stride,
+                           const unsigned* index, size_t sz, size_t nstripes,
+                           const int* devices, size_t ndevices, unsigned flags);
 
 /* Page-locked host memory (hipHostMalloc): host buffers passed to fec_encode /
  * fec_decode from here are read and written by the kernel in place (no
@@ -191,6 +217,14 @@ int fec_generic_mode(int mode);
 
 /* Wait for background compiles; returns the number of compiled kernels. */
 int fec_jit_wait(void);
+
+/* Diagnostics and A/B runs.  The ZFEC_HIP_* environment knobs are read once,
+ * at the library's first call; fec_reload_config re-reads them (returns
+ * FEC_OK).  fec_last_wait: how the calling thread's last synchronous
+ * small-object call waited for its kernel -- 1 = on the completion word the
+ * kernel itself wrote to pinned host memory, 0 = hipStreamSynchronize. */
+int fec_reload_config(void);
+int fec_last_wait(void);
 
 /* Compile now (no GPU needed) the kernels an fec_encode of block_nums, or an
  * fec_decode from `index` (flags as fec_decode_ex), would use.  FEC_OK, or

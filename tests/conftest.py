@@ -21,3 +21,20 @@ def golden():
         meta = json.load(f)
     arrays = dict(np.load(os.path.join(d, "golden.npz"), allow_pickle=False))
     return meta, arrays
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    """Set ZFEC_HIP_* environment knobs for one test.  The library reads them
+    once per process, so they are re-read (fec_reload_config) after being set
+    and again after the test has restored the environment."""
+    from zfec_amd import capi
+
+    def set_knobs(**kv):
+        for key, val in kv.items():
+            monkeypatch.setenv(key, str(val))
+        capi.reload_config()
+
+    yield set_knobs
+    monkeypatch.undo()
+    capi.reload_config()

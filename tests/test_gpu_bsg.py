@@ -4,10 +4,12 @@ every wide-code launch no compiled JIT kernel serves -- above all decodes of an
 erasure pattern seen for the first time (zfec/fec.c:527-557 decodes every
 pattern with one code path).  Bit-exact against the CPU oracle across code
 shapes (every rows-per-wave instantiation, rows not a multiple of 4, k up to
-32), block sizes around the 4 KiB unit and its overlapping last unit, both
-phase depths (ZFEC_HIP_BSG_PHASE) and scheduling variants (ZFEC_HIP_BSG_SB), batched strided stripes at misaligned
-bases with guard bytes, and random erasure patterns."""
-import os
+32), block sizes around the 4 KiB unit and its overlapping last unit, batched
+strided stripes at misaligned bases with guard bytes, and random erasure
+patterns; and codes of more than 32 inputs in one pass, their block pointers
+and coefficients read from a device-side table (the reference takes any
+1 <= k <= m <= 256, zfec/fec.c:437-440; its own benchmark times 94/100,
+benchmark-zfec/Main.hs:17)."""
 
 import numpy as np
 import pytest
@@ -27,21 +29,13 @@ def need_gpu():
         pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
 
 
-@pytest.fixture(params=[("2", "0", "0"), ("4", "0", "0"), ("2", "1", "0"), ("2", "0", "1")],
-                ids=["phase2", "phase4", "phase2_sb", "phase2_bb"])
-def bsg_only(request):
+@pytest.fixture
+def bsg_only(knobs):
     """JIT off, generic kernel on, matapply_small off (these small launches
-    would take it); the variant knobs are read per launch."""
+    would take it)."""
     prev_j, prev_g = capi.jit_mode(capi.JIT_OFF), capi.generic_mode(1)
-    keys = ("ZFEC_HIP_BSG_PHASE", "ZFEC_HIP_BSG_SB", "ZFEC_HIP_BSG_BB", "ZFEC_HIP_SMALL_LANES")
-    old = {key: os.environ.get(key) for key in keys}
-    os.environ.update(dict(zip(keys, tuple(request.param) + ("0",))))
+    knobs(ZFEC_HIP_SMALL_LANES=0)
     yield
-    for key, val in old.items():
-        if val is None:
-            os.environ.pop(key, None)
-        else:
-            os.environ[key] = val
     capi.jit_mode(prev_j)
     capi.generic_mode(prev_g)
 
@@ -157,3 +151,77 @@ def test_bsg_off_gives_identical_bytes():
     finally:
         capi.jit_mode(prev_j)
     assert torch.equal(outs[0], outs[1])
+
+
+# k > 32: one pass with the device-side table (r <= 48 per launch; wider r in
+# near-equal row groups), instead of XOR-accumulating passes of 32 inputs
+WIDE_SHAPES = [(33, 41), (47, 60), (94, 100), (64, 112), (128, 150), (200, 256), (255, 256)]
+
+
+@pytest.mark.parametrize("k,m", WIDE_SHAPES)
+def test_bsg_wide_k_vs_oracle(bsg_only, k, m):
+    rng = np.random.default_rng(k * 1000 + m)
+    for sz in (4096, 6001):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name().startswith("matapply_bsg") and capi.last_kernel_name().endswith(",tbl>"), \
+            capi.last_kernel_name()
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        # decode from a random k of the m blocks
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz, nums)
+
+
+def test_bsg_wide_k_batched_guards(bsg_only):
+    """94/100 over strided stripes at misaligned bases: every stripe against the
+    oracle, bytes between rows and around the buffer untouched; the same batch
+    again with the generic kernel off (XOR-accumulating table passes) gives the
+    same bytes."""
+    k, m, sz, ns = 94, 100, 5000, 5
+    r = m - k
+    rng = np.random.default_rng(94)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    ld = sz + 40
+    src = torch.zeros(7 + ns * k * ld, dtype=torch.uint8, device="cuda")
+    src[7:].view(ns, k, ld)[:, :, :sz] = torch.from_numpy(data).cuda()
+    outs = []
+    for gen in (1, 0):
+        capi.generic_mode(gen)
+        dst = torch.full((9 + ns * r * ld + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        code = capi.Code(k, m)
+        code.encode_batch(src.data_ptr() + 7, ld, k * ld, dst.data_ptr() + 9, ld, r * ld, list(range(k, m)), sz, ns,
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name().startswith("matapply_bsg" if gen else "matapply_lds"), capi.last_kernel_name()
+        outs.append(dst.cpu().numpy())
+    capi.generic_mode(1)
+    assert np.array_equal(outs[0], outs[1])
+    d = outs[0]
+    assert (d[:9] == 0xA5).all() and (d[9 + ns * r * ld:] == 0xA5).all()
+    o = d[9:9 + ns * r * ld].reshape(ns, r, ld)
+    assert (o[:, :, sz:] == 0xA5).all(), "write past a row"
+    for s_ in range(ns):
+        assert (o[s_, :, :sz] == oracle.encode(k, m, data[s_])).all(), s_
+
+
+def test_bsg_wide_k_table_ring_reuse(bsg_only):
+    """More wide launches than the table ring has slots, queued back to back on
+    one stream with different matrices (every decode pattern a new one): each
+    launch must read its own table, so every result is checked."""
+    k, m, sz = 40, 60, 8192
+    rng = np.random.default_rng(40)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    allb = zfec_amd.Encoder(k, m).encode(ins)
+    dec = zfec_amd.Decoder(k, m)
+    results = []
+    for _ in range(20):  # 20 > 8 ring slots
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        results.append((nums, dec.decode([allb[n] for n in nums], nums)))
+    torch.cuda.synchronize()
+    for nums, got in results:
+        assert (torch.stack(got).cpu().numpy() == data).all(), nums

@@ -246,13 +246,12 @@ def test_c_abi_host_memory_flag():
 
 @pytest.mark.parametrize("env", [{"ZFEC_HIP_POOL_COPY_MIN": "0"}, {"ZFEC_HIP_STAGE_MIN": str(1 << 60)},
                                  {"ZFEC_HIP_STAGE_MIN": "0"}])
-def test_host_small_call_paths(env, monkeypatch):
+def test_host_small_call_paths(env, knobs):
     """Host calls under 4 MiB: the pinned bounce buffer with its copies on the
     host pool, the bounce buffer up to 4 MiB (staged path off), and the staged
     path from any size (blocks >= 64 KiB) -- each bit-exact against the oracle,
     encode and a mixed primary/secondary decode."""
-    for key, val in env.items():
-        monkeypatch.setenv(key, val)
+    knobs(**env)
     k, m = 3, 10
     rng = np.random.default_rng(77)
     for sz in [65536, 70_001, 349_525, 1_000_003]:
@@ -544,14 +543,13 @@ def _run_child(spec, env_extra, tmp_path, tag):
 
 @pytest.mark.parametrize("layout", sorted(_LAYOUTS))
 def test_batch_layout_env_variants(layout, tmp_path):
-    """The same fec_encode_batch run six ways, each in its own process since
-    the knobs are read once: as shipped, with the block-major collapse off
-    (ZFEC_HIP_BATCH_COLLAPSE=0), with at most 1024 units per launch
+    """The same fec_encode_batch run five ways, each in its own process (the
+    knobs are read once per process): as shipped, with the block-major collapse
+    off (ZFEC_HIP_BATCH_COLLAPSE=0), with at most 1024 units per launch
     (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte ranges, batches
-    into stripe groups), with the register kernels' store policy forced to nt
-    and to nt sc1 (ZFEC_HIP_STORE), and with the row walk taking one piece at
-    a time (ZFEC_HIP_ROWS_PRE=0).  All outputs, guard bytes included, must be
-    identical, and sampled stripes must equal the oracle's parity."""
+    into stripe groups), and with the register kernels' store policy forced to
+    nt and to nt sc1 (ZFEC_HIP_STORE).  All outputs, guard bytes included,
+    must be identical, and sampled stripes must equal the oracle's parity."""
     import importlib.util
     import os
 
@@ -566,8 +564,6 @@ def test_batch_layout_env_variants(layout, tmp_path):
         assert np.array_equal(base, got), "store policy %s changed the output" % pol
     if layout == "rows_object_major":
         assert "matapply_rows" in kern, kern
-    one, _ = _run_child(spec, {"ZFEC_HIP_ROWS_PRE": "0"}, tmp_path, "rows_one_piece")
-    assert np.array_equal(base, one), "the one-piece row walk changed the output"
     child = importlib.util.spec_from_file_location(
         "gpu_batch_child", os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpu_batch_child.py"))
     mod = importlib.util.module_from_spec(child)
@@ -626,7 +622,9 @@ def test_batch_short_rows_walk(k, m, sz, ns, rows):
 
 @pytest.mark.parametrize("k,m,sz,ns,ld,used", [(3, 10, 1366, 300, 1536, True), (3, 10, 1366, 300, 1400, False),
                                                (2, 6, 5000, 20, 5120, True), (3, 10, 1408, 100, 1536, True),
-                                               (3, 10, 777, 3, 1024, True), (20, 60, 1000, 8, 1024, True)])
+                                               (3, 10, 777, 3, 1024, True), (20, 60, 1000, 8, 1024, True),
+                                               (3, 10, 100_003, 1, 100_096, True), (3, 10, 100_003, 1, 100_100, False),
+                                               (10, 16, 70_001, 1, 70_144, True)])
 def test_batch_row_padding_flag(k, m, sz, ns, ld, used):
     """FEC_FLAG_ROW_PADDING: the library may run each row out to its next
     128-byte line.  Bytes [0, sz) stay bit-exact against the oracle; bytes from
@@ -899,18 +897,15 @@ def test_tensor_batch_api(k, m, sz, ns, block_major):
             zfec_amd.Decoder(k, m).decode_batch(recv, bad)  # primary off its slot
 
 
-@pytest.mark.parametrize("path,chunk", [("stage", None), ("stage", 65536), ("stage", 3 << 20),
-                                        ("lock", None), ("lock", 65536), ("lock", 3 << 20), ("copy", None)])
-def test_large_pageable_bytes_path(path, chunk, monkeypatch):
-    """Large pageable host blocks (bytes / numpy views sharing pages) take one
-    of the host paths (fec_abi.cpp): staged through pinned slots by the host
-    copy threads (run_staged, the default), page-locked chunk by chunk
-    (run_pageable) or the DMA pipeline (run_pipeline).  Parity and a
-    secondary-only decode bit-exact against the oracle, at the default chunk
-    and at chunk sizes that cut blocks at odd page offsets."""
-    monkeypatch.setenv("ZFEC_HIP_HOST_PATH", path)
+@pytest.mark.parametrize("chunk", [None, 65536, 3 << 20])
+def test_large_pageable_bytes_path(chunk, knobs):
+    """Large pageable host blocks (bytes / numpy views sharing pages) are
+    staged through pinned slots by the host copy threads (fec_abi.cpp
+    run_staged).  Parity and a secondary-only decode bit-exact against the
+    oracle, at the default chunk and at chunk sizes that cut blocks at odd page
+    offsets (ZFEC_HIP_STAGE_CHUNK)."""
     if chunk:
-        monkeypatch.setenv("ZFEC_HIP_PAGEABLE_CHUNK" if path == "lock" else "ZFEC_HIP_STAGE_CHUNK", str(chunk))
+        knobs(ZFEC_HIP_STAGE_CHUNK=chunk)
     k, m, sz = 3, 10, (5 << 20) + 123
     rng = np.random.default_rng(sz)
     flat = rng.integers(0, 256, size=k * sz, dtype=np.uint8)
@@ -1078,3 +1073,74 @@ def test_batch_api_host_numpy_arrays():
         recv = np.stack([par[:, 4], data[:, 1], par[:, 6]], axis=1)
         rec = dec.decode_batch(recv, nums)
         assert (rec == data[:, [0, 2], :]).all()
+
+
+def test_bench_headline_call_vs_oracle():
+    """The exact calls bench.py times for its headline (BASELINE configs[1],
+    bench.py run_workload): ONE K=3/M=10 stripe of sz = ceil(64 MiB / 3) =
+    22,369,622-byte blocks in 22,369,792-byte rows, fec_encode_batch and then
+    fec_decode_batch from blocks 7, 8, 9, both with FEC_FLAG_ASYNC |
+    FEC_FLAG_ROW_PADDING on a torch stream -- the single-stripe padding grant
+    (fec_abi.cpp run_batch) on the nt sc1 register kernels.  Bytes [0, sz)
+    against the oracle on slices at the start, middle and end of the blocks
+    (every output byte depends only on the same column of the inputs,
+    zfec/fec.c:494-503); the bytes past roundup(sz, 128) up to the row stride
+    are guard bytes that must stay untouched."""
+    k, m = 3, 10
+    r = m - k
+    sz = -(-(64 << 20) // k)
+    ld = -(-sz // 256) * 256
+    pad = -(-sz // 128) * 128
+    assert (sz, ld) == (22_369_622, 22_369_792)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    data = torch.randint(0, 256, (1, k, ld), dtype=torch.uint8, device="cuda", generator=g)
+    par = torch.full((1, r, ld), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    fl = capi.FEC_FLAG_ASYNC | capi.FEC_FLAG_ROW_PADDING
+    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, 1, stream=st,
+                      flags=fl)
+    assert capi.last_kernel_name() == "matapply_reg<3,7>", capi.last_kernel_name()
+    torch.cuda.synchronize()
+    assert bool((par[:, :, pad:] == 0xA5).all()), "encode wrote past the padded row end"
+    L = 1 << 20
+    for c0 in (0, sz // 2 - L // 2 + 13, sz - L):
+        ins = data[0, :, c0:c0 + L].cpu().numpy()
+        assert (par[0, :, c0:c0 + L].cpu().numpy() == oracle.encode(k, m, ins)).all(), c0
+    # decode from blocks 7, 8, 9 (all secondaries): the received rows as the bench stages them
+    slots = [7, 8, 9]
+    recv = torch.stack([par[0, s - k] for s in slots]).unsqueeze(0).contiguous()
+    rec = torch.full((1, k, ld), 0xA5, dtype=torch.uint8, device="cuda")
+    code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, k * ld, slots, sz, 1, stream=st, flags=fl)
+    assert capi.last_kernel_name() == "matapply_reg<3,3>", capi.last_kernel_name()
+    torch.cuda.synchronize()
+    assert bool(torch.equal(rec[:, :, :sz], data[:, :, :sz])), "decode(encode(x)) != x"
+    assert bool((rec[:, :, pad:] == 0xA5).all()), "decode wrote past the padded row end"
+    for c0 in (0, sz - L):
+        got = rec[0, :, c0:c0 + L].cpu().numpy()
+        want = oracle.decode(k, m, recv[0, :, c0:c0 + L].cpu().numpy(), slots)
+        assert (got == want).all(), c0
+
+
+@pytest.mark.parametrize("mode", ["signal", "sync"])
+def test_small_call_wait_modes(mode, knobs):
+    """4 KiB K=3/M=10 stripes from Python bytes: the one-workgroup register
+    kernel publishes its completion in pinned host memory and the caller spins
+    on it (fec_abi.cpp run_single); ZFEC_HIP_WAIT=sync waits in
+    hipStreamSynchronize instead.  Both bit-exact against the oracle, and the
+    path actually taken is the one asked for (fec_last_wait)."""
+    if mode == "sync":
+        knobs(ZFEC_HIP_WAIT="sync")
+    k, m = 3, 10
+    rng = np.random.default_rng(4096)
+    enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+    for sz in (1366, 4096, 1):
+        for _ in range(20):
+            data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+            out = enc.encode([data[i].tobytes() for i in range(k)])
+            assert capi.last_wait() == (1 if mode == "signal" else 0), (mode, sz)
+            par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+            assert (par == oracle.encode(k, m, data)).all(), sz
+            rec = dec.decode([out[7], out[1], out[9]], [7, 1, 9])
+            assert capi.last_wait() == (1 if mode == "signal" else 0), (mode, sz)
+            assert b"".join(rec) == data.tobytes(), sz

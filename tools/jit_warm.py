@@ -21,8 +21,9 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-# (k, m): tests/test_gpu_jit.py shapes, the auto-policy shape, bench cfg3 / cfg4
-SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (10, 58), (4, 12), (12, 21)]
+# (k, m): tests/test_gpu_jit.py shapes, the auto-policy shape, bench cfg3 / cfg4, the wide-k shapes
+SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (10, 58), (4, 12), (12, 21), (94, 100),
+          (40, 48)]
 
 
 def main():

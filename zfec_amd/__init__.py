@@ -152,6 +152,26 @@ class _as_error(object):
         return False
 
 
+def _devices_arg(blocks, devices):
+    """None, or the list of devices a host-array batch is split over
+    ("all": every visible GPU).  Device tensors stay on their own device."""
+    if devices is None:
+        return None
+    if isinstance(devices, str):
+        if devices != "all":
+            raise Error("Precondition violation: devices is required to be a list of device indices or 'all'")
+        devices = list(range(device_count()))
+    devs = [int(d) for d in devices]
+    if not devs:
+        raise Error("Precondition violation: devices is required to list at least one device")
+    if not _is_host_array(blocks):
+        if devs != [blocks.device.index if blocks.device.index is not None else 0]:
+            raise Error("Precondition violation: a device tensor batch runs on its own device; devices= splits host "
+                        "(numpy) batches over several GPUs")
+        return None
+    return devs
+
+
 def _capi_code(coder):
     code = getattr(coder, "_batch_code", None)
     if code is None:
@@ -174,19 +194,26 @@ class Encoder(_fec.Encoder):
             return _fec.Encoder.encode(self, inblocks, desired_blocks_nums)
         return self._encode_device(list(inblocks), desired_blocks_nums)
 
-    def encode_batch(self, blocks, desired_blocks_nums=None):
+    def encode_batch(self, blocks, desired_blocks_nums=None, devices=None):
         """Encode many independent stripes in one launch (fec_encode_batch).
 
         blocks: uint8 device tensor [nstripes, k, sz] (any strides with unit
         stride along sz; a transposed block-major [k, nstripes, sz] array is the
-        fastest layout), or the same as a host numpy array.  desired_blocks_nums:
-        secondary block numbers in [k, m-1] (default k..m-1).  Returns a new
-        [nstripes, len(desired), sz] tensor (numpy array for host input),
-        block-major when the input was; device work is enqueued on the current
-        stream, host calls return when done.  A batched counterpart of encode() for many small objects
-        (SURVEY.md §8f row 2); no reference equivalent."""
+        fastest layout), or the same as a host numpy array, or a list of such
+        device tensors (one per GPU: each runs on its own device, and a list of
+        results comes back).  desired_blocks_nums: secondary block numbers in
+        [k, m-1] (default k..m-1).  devices (host arrays only): a list of GPU
+        indices, or "all", to split the stripes over (fec_encode_batch_multi:
+        one library thread per GPU, each staging its share over its own PCIe
+        link).  Returns a new [nstripes, len(desired), sz] tensor (numpy array
+        for host input), block-major when the input was; device work is
+        enqueued on the current stream, host calls return when done.  A batched
+        counterpart of encode() for many small objects (SURVEY.md §8f row 2);
+        no reference equivalent."""
         from . import capi
 
+        if isinstance(blocks, (list, tuple)):
+            return [self.encode_batch(b, desired_blocks_nums) for b in blocks]
         k, m = self.k, self.m
         nums = list(range(k, m)) if desired_blocks_nums is None else list(desired_blocks_nums)
         for x in nums:
@@ -194,12 +221,17 @@ class Encoder(_fec.Encoder):
                 raise Error("Precondition violation: encode_batch desired block nums are required to be secondary "
                             "block nums in [k, m-1] = [%d, %d], but one was %r" % (k, m - 1, x))
         ns, sz, sbs, sss, ptr = _batch_view(blocks, k, "blocks")
+        devs = _devices_arg(blocks, devices)
         out = _batch_out(blocks, sss < sbs, ns, len(nums), sz)
         if nums and ns and sz:
             optr, obs, oss = _batch_strides(out)
-            stream, flags = _batch_call_args(blocks)
             with _as_error():
-                _capi_code(self).encode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream, flags=flags)
+                if devs is not None:
+                    _capi_code(self).encode_batch_multi(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, devs)
+                else:
+                    stream, flags = _batch_call_args(blocks)
+                    _capi_code(self).encode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream,
+                                                  flags=flags)
         return out
 
     def _encode_device(self, inblocks, desired):
@@ -244,18 +276,21 @@ class Decoder(_fec.Decoder):
             return _fec.Decoder.decode(self, blocks, blocknums)
         return self._decode_device(list(blocks), blocknums)
 
-    def decode_batch(self, blocks, blocknums):
+    def decode_batch(self, blocks, blocknums, devices=None):
         """Decode many independent stripes that all received the same block
         numbers, in one launch (fec_decode_batch).
 
         blocks: uint8 device tensor or host numpy array [nstripes, k, sz]
-        (strides as in Encoder.encode_batch), slot j of every stripe holding
-        block blocknums[j];
+        (strides as in Encoder.encode_batch), or a list of device tensors (one
+        per GPU), slot j of every stripe holding block blocknums[j];
         a primary block must sit at its own slot (primary i at slot i, as
-        fec_decode requires, zfec/fec.c:549).  Returns a new [nstripes, r, sz]
-        tensor of the r missing primaries in ascending order."""
+        fec_decode requires, zfec/fec.c:549).  devices: as in
+        Encoder.encode_batch (fec_decode_batch_multi).  Returns a new
+        [nstripes, r, sz] tensor of the r missing primaries in ascending order."""
         from . import capi
 
+        if isinstance(blocks, (list, tuple)):
+            return [self.decode_batch(b, blocknums) for b in blocks]
         k, m = self.k, self.m
         try:
             nums = list(blocknums)
@@ -270,13 +305,18 @@ class Decoder(_fec.Decoder):
             if x < k and x != i:
                 raise Error("Precondition violation: decode_batch requires primary block %d at slot %d" % (x, x))
         ns, sz, sbs, sss, ptr = _batch_view(blocks, k, "blocks")
+        devs = _devices_arg(blocks, devices)
         r = sum(1 for x in nums if x >= k)
         out = _batch_out(blocks, sss < sbs, ns, r, sz)
         if r and ns and sz:
             optr, obs, oss = _batch_strides(out)
-            stream, flags = _batch_call_args(blocks)
             with _as_error():
-                _capi_code(self).decode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream, flags=flags)
+                if devs is not None:
+                    _capi_code(self).decode_batch_multi(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, devs)
+                else:
+                    stream, flags = _batch_call_args(blocks)
+                    _capi_code(self).decode_batch(ptr, sbs, sss, optr, obs, oss, nums, sz, ns, stream=stream,
+                                                  flags=flags)
         return out
 
     def _check_blocknums(self, blocknums):

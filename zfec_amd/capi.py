@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzfec_hip.so")
+# ZFEC_HIP_LIB: another build of the library (make asan-py: the host code built
+# with AddressSanitizer); the default is the in-tree build next to this file
+LIB_PATH = os.environ.get("ZFEC_HIP_LIB") or os.path.join(_HERE, "libzfec_hip.so")
 
 FEC_OK, FEC_EINVAL, FEC_ENODEV, FEC_EHIP, FEC_ENOMEM, FEC_ESINGULAR, FEC_EUNINIT = range(7)
 FEC_FLAG_ASYNC = 1
@@ -24,6 +26,7 @@ _SZ = ctypes.c_size_t
 _U = ctypes.c_uint
 _UP = ctypes.POINTER(ctypes.c_uint)
 _PP = ctypes.POINTER(ctypes.c_void_p)
+_IP = ctypes.POINTER(ctypes.c_int)
 SYMBOLS = [
     ("fec_init", None, []),
     ("fec_new", _P, [ctypes.c_ushort, ctypes.c_ushort]),
@@ -49,6 +52,10 @@ SYMBOLS = [
     ("fec_generic_mode", ctypes.c_int, [ctypes.c_int]),
     ("fec_jit_prepare_encode", ctypes.c_int, [_P, _UP, _SZ]),
     ("fec_jit_prepare_decode", ctypes.c_int, [_P, _UP, _U]),
+    ("fec_encode_batch_multi", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _SZ, _IP, _SZ, _U]),
+    ("fec_decode_batch_multi", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _IP, _SZ, _U]),
+    ("fec_reload_config", ctypes.c_int, []),
+    ("fec_last_wait", ctypes.c_int, []),
 ]
 
 JIT_OFF, JIT_AUTO, JIT_FORCE = 0, 1, 2
@@ -117,6 +124,18 @@ def jit_wait():
     return lib().fec_jit_wait()
 
 
+def reload_config():
+    """Re-read the ZFEC_HIP_* environment knobs (read once per process
+    otherwise; tests and A/B runs)."""
+    check(lib().fec_reload_config())
+
+
+def last_wait():
+    """1 if the calling thread's last synchronous small-object call waited on
+    the completion word its kernel wrote, 0 if on hipStreamSynchronize."""
+    return lib().fec_last_wait()
+
+
 def ptr_array(addrs):
     return (ctypes.c_void_p * max(1, len(addrs)))(*addrs)
 
@@ -156,6 +175,18 @@ class Code(object):
     def decode_batch(self, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
         check(lib().fec_decode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(index),
                                      sz, nstripes, stream or None, flags))
+
+    def encode_batch_multi(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, devices, flags=0):
+        """fec_encode_batch_multi: the stripes split over `devices` (host memory)."""
+        devs = (ctypes.c_int * max(1, len(devices)))(*devices)
+        check(lib().fec_encode_batch_multi(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(block_nums),
+                                           len(block_nums), sz, nstripes, devs, len(devices), flags))
+
+    def decode_batch_multi(self, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, devices, flags=0):
+        """fec_decode_batch_multi: the stripes split over `devices` (host memory)."""
+        devs = (ctypes.c_int * max(1, len(devices)))(*devices)
+        check(lib().fec_decode_batch_multi(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(index), sz, nstripes,
+                                           devs, len(devices), flags))
 
     def encode_ptrs(self, in_addrs, out_addrs, block_nums, sz, stream=0, flags=FEC_FLAG_ASYNC):
         check(lib().fec_encode_ex(self.ptr, ptr_array(in_addrs), ptr_array(out_addrs), uint_array(block_nums),

@@ -37,6 +37,7 @@
 
 #include <hip/hiprtc.h>
 
+#include "config.hpp"
 #include "gf256.hpp"
 
 namespace zfec_hip {
@@ -231,14 +232,28 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // share: each wave of the workgroup loads and transposes k / ntiles of the
     // unit's inputs once and leaves their bit-planes in LDS for all waves
     const bool share = split && opt.share;
+    // probe 1 (no HBM traffic): an input is synthesised from the lane, the
+    // unit and the block number instead of loaded
+    const unsigned probe = opt.probe;
+    auto emit_ld = [&](const char* ind, const char* dst, const char* rsrc, unsigned j) {
+        if (probe == 1)
+            e("%sconst u32x4 %s_0 = u32x4{lo16 ^ (u32)ub, %uu, (u32)ub, lo16 + %uu}, %s_1 = u32x4{(u32)ub + %uu, lo16, "
+              "%uu ^ (u32)ub, lo16 * %uu};\n",
+              ind, dst, j * 2654435761u, j, dst, j * 40503u, j + 7, 2 * j + 1);
+        else
+            e("%sconst u32x4 %s_0 = ld(%s, lo16), %s_1 = ld(%s, lo16 + 1024u);\n", ind, dst, rsrc, dst, rsrc);
+    };
     auto emit_load = [&](unsigned n) {
         const unsigned j = n % k;
         if (share) {
             e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, j * 128, n, j * 128 + 64);
             return;
         }
-        e("    const __amdgpu_buffer_rsrc_t ri%u = rs(%sin[%u] + ub);\n", n, PA, j);
-        e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", n, n, n, n);
+        char dst[16], rsrc[16];
+        snprintf(dst, sizeof dst, "l%u", n);
+        snprintf(rsrc, sizeof rsrc, "ri%u", n);
+        if (probe != 1) e("    const __amdgpu_buffer_rsrc_t ri%u = rs(%sin[%u] + ub);\n", n, PA, j);
+        emit_ld("    ", dst, rsrc, j);
     };
     if (!split)
         for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
@@ -249,15 +264,19 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             e("    if (tile == %uu) {\n", t);
             launder("      ");
             for (unsigned j = t; j < k; j += ntiles) {
-                e("      const __amdgpu_buffer_rsrc_t pi%u = rs(%sin[%u] + ub);\n", j, PA, j);
-                e("      const u32x4 p%u_0 = ld(pi%u, lo16), p%u_1 = ld(pi%u, lo16 + 1024u);\n", j, j, j, j);
+                char dst[16], rsrc[16];
+                snprintf(dst, sizeof dst, "p%u", j);
+                snprintf(rsrc, sizeof rsrc, "pi%u", j);
+                if (probe != 1) e("      const __amdgpu_buffer_rsrc_t pi%u = rs(%sin[%u] + ub);\n", j, PA, j);
+                emit_ld("      ", dst, rsrc, j);
             }
             for (unsigned j = t; j < k; j += ntiles) {
                 e("      u32 w%u_0 = p%u_0.x, w%u_1 = p%u_0.y, w%u_2 = p%u_0.z, w%u_3 = p%u_0.w;\n", j, j, j, j, j, j, j,
                   j);
                 e("      u32 w%u_4 = p%u_1.x, w%u_5 = p%u_1.y, w%u_6 = p%u_1.z, w%u_7 = p%u_1.w;\n", j, j, j, j, j, j, j,
                   j);
-                e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
+                if (probe != 2)
+                    e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
                 e("      sh[%uu + lane] = u32x4{w%u_0, w%u_1, w%u_2, w%u_3};\n", j * 128, j, j, j, j);
                 e("      sh[%uu + lane] = u32x4{w%u_4, w%u_5, w%u_6, w%u_7};\n", j * 128 + 64, j, j, j, j);
             }
@@ -285,6 +304,18 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                 emit_load(n + pf);
             e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", n, n, n, n, n, n, n, n);
             e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", n, n, n, n, n, n, n, n);
+            if (probe == 2) {  // no arithmetic: one XOR per plane into the tile's first row
+                for (unsigned b = 0; b < 8; ++b) {
+                    char& ini = init[b];
+                    if (!ini)
+                        e("    a%u_%u = q%u_%u;\n", r0, b, n, b);
+                    else
+                        e("    a%u_%u ^= q%u_%u;\n", r0, b, n, b);
+                    ini = 1;
+                }
+                if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
+                continue;
+            }
             if (!share)  // LDS holds planes already
                 e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
             Combos lo{n, 'L', 0}, hi{n, 'H', 4};
@@ -349,12 +380,22 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
         }
         for (unsigned i = r0; i < r1; ++i) {
-            for (unsigned b = 0; b < 8; ++b)
-                if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
-            e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
+            if (probe == 2 && i > r0) {
+                e("    a%u_0 = a%u_0 ^ %uu;", i, r0, i);
+                for (unsigned b = 1; b < 8; ++b) e(" a%u_%u = a%u_%u;", i, b, r0, b);
+                e("\n");
+            } else {
+                for (unsigned b = 0; b < 8; ++b)
+                    if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
+            }
+            if (probe != 2)
+                e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
+            const char* guard = probe == 1 ? "    if (a%u_0 == 0x9E3779B9u && a%u_5 == 0x7F4A7C15u) {\n" : nullptr;
+            if (guard) e(guard, i, i);
             e("    const __amdgpu_buffer_rsrc_t ro%u = rs(%sout[%u] + uo);\n", i, PA, i);
             e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
             e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
+            if (guard) e("    }\n");
         }
         if (split) e("    }\n");
     }
@@ -572,26 +613,11 @@ void run_compile(Entry* e, std::string src) {
 
 std::atomic<int> g_mode{-1};
 
-unsigned env_uint(const char* name, unsigned dflt) {
-    const char* v = getenv(name);
-    return v && *v ? static_cast<unsigned>(strtoul(v, nullptr, 10)) : dflt;
-}
-
-BsOptions options_from_env() {
-    BsOptions o;
-    o.max_tile = env_uint("ZFEC_HIP_JIT_TILE", o.max_tile);
-    if (o.max_tile == 0 || o.max_tile > 32) o.max_tile = kBsMaxTile;
-    o.prefetch = env_uint("ZFEC_HIP_JIT_PREFETCH", o.prefetch);
-    if (o.prefetch > 4) o.prefetch = 4;
-    o.barriers = env_uint("ZFEC_HIP_JIT_BARRIER", 1) != 0;
-    o.store_aux = env_uint("ZFEC_HIP_JIT_STORE", o.store_aux) & 0x1Fu;
-    o.gray = env_uint("ZFEC_HIP_JIT_ORDER", o.gray ? 1 : 0) != 0;
-    o.waves = env_uint("ZFEC_HIP_JIT_WAVES", o.waves);
-    o.split = env_uint("ZFEC_HIP_JIT_SPLIT", o.split ? 1 : 0) != 0;
-    o.share = env_uint("ZFEC_HIP_JIT_SHARE", o.share ? 1 : 0) != 0;
-    o.argload = env_uint("ZFEC_HIP_JIT_ARGLOAD", o.argload ? 1 : 0) != 0;
-    o.shift64 = env_uint("ZFEC_HIP_JIT_SHIFT64", o.shift64 ? 1 : 0) != 0;
-    if (o.waves > 8) o.waves = 8;
+// Options of a kernel for an r x k matrix: the configured ones, with the
+// planes shared through LDS only while all k inputs' planes fit (2 KiB each).
+BsOptions options_for(unsigned k) {
+    BsOptions o = config().jit;
+    if (k > 32) o.share = false;
     return o;
 }
 
@@ -599,21 +625,22 @@ BsOptions options_from_env() {
 // with R.mu held by `lk`; releases it while compiling synchronously.
 std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt) {
     std::string key;
-    key.reserve(48 + size_t(k) * r);
-    char hdr[64];
+    key.reserve(64 + size_t(k) * r);
+    char hdr[80];
     snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
              opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
     key += hdr;
     if (opt.argload) key += "argload/";
     if (opt.shift64) key += "shift64/";
     if (opt.share && bitslice_split(r, opt)) key += "share/";
+    if (opt.probe) key += "probe" + std::to_string(opt.probe) + "/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;
 }
 
 Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
     Registry& R = reg();
-    const BsOptions opt = options_from_env();
+    const BsOptions opt = options_for(k);
     const std::string key = entry_key(coef, k, r, opt);
     auto it = R.entries.find(key);
     if (it != R.entries.end()) return it->second.get();
@@ -641,16 +668,16 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     return e;
 }
 
-// The table kernels serve the rest: few coefficients (memory-bound), blocks
-// shorter than one unit, XOR-accumulating continuation passes, small launches
-// (auto mode).
-bool eligible(const MatJob& job, JitMode mode) {
-    if (mode == kJitOff || job.accumulate || job.tables || job.sz < static_cast<uint64_t>(kBsChunk) ||
-        job.nstripes == 0 || job.k == 0 || job.r == 0)
+// The other kernels serve the rest: few coefficients (memory-bound), blocks
+// shorter than one unit, XOR-accumulating continuation passes, matrices past
+// kJitMaxCoef, small launches (auto mode).
+bool eligible(const ApplySpec& a, JitMode mode) {
+    if (mode == kJitOff || a.accumulate || a.sz < static_cast<uint64_t>(kBsChunk) || a.nstripes == 0 || a.k == 0 ||
+        a.r == 0 || a.k * a.r > kJitMaxCoef)
         return false;
     if (mode == kJitForce) return true;
-    if (job.k * job.r < 24 || (job.k <= 4 && job.r <= 8)) return false;
-    const double bytes = double(job.k + job.r) * double(job.sz) * double(job.nstripes);
+    if (a.k * a.r < 24 || (a.k <= 4 && a.r <= 8)) return false;
+    const double bytes = double(a.k + a.r) * double(a.sz) * double(a.nstripes);
     return bytes >= double(8u << 20);
 }
 
@@ -659,6 +686,22 @@ bool eligible(const MatJob& job, JitMode mode) {
 // kAutoMaxKernels matrices in all.
 constexpr int kAutoMinUses = 2;
 constexpr size_t kAutoMaxKernels = 512;
+
+// A thread's recent launches of ready kernels: the next launch of the same
+// matrix on the same device (and configuration) skips the registry's lock,
+// key string and map lookups.
+struct Hit {
+    const Config* cfg = nullptr;
+    int dev = -1;
+    unsigned k = 0, r = 0;
+    std::vector<uint8_t> coef;
+    Loaded L;
+    const char* name = nullptr;
+    unsigned threads = 0, upb = 0;
+};
+constexpr int kHits = 4;
+thread_local Hit t_hits[kHits];
+thread_local unsigned t_hit_next = 0;
 
 }  // namespace
 
@@ -669,7 +712,8 @@ JitMode jit_mode() {
         m = kJitAuto;
         if (e && (!strcmp(e, "0") || !strcmp(e, "off"))) m = kJitOff;
         if (e && (!strcmp(e, "2") || !strcmp(e, "force"))) m = kJitForce;
-        g_mode.store(m);
+        int expect = -1;
+        if (!g_mode.compare_exchange_strong(expect, m)) m = expect;  // set_jit_mode won the race
     }
     return static_cast<JitMode>(m);
 }
@@ -677,7 +721,7 @@ JitMode jit_mode() {
 void set_jit_mode(JitMode m) { g_mode.store(static_cast<int>(m)); }
 
 int jit_prepare(const uint8_t* coef, unsigned k, unsigned r) {
-    if (k == 0 || r == 0) return -1;
+    if (k == 0 || r == 0 || k * r > kJitMaxCoef) return -1;
     Registry& R = reg();
     std::unique_lock<std::mutex> lk(R.mu);
     Entry* e = get_entry(coef, k, r, true, lk);
@@ -698,75 +742,110 @@ std::string jit_last_error() {
     return R.last_error;
 }
 
-hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char** name_out) {
+hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const char** name_out) {
     const JitMode mode = jit_mode();
-    if (!eligible(job, mode)) return hipErrorNotSupported;
-    Registry& R = reg();
-    std::unique_lock<std::mutex> lk(R.mu);
-    if (mode == kJitAuto) {
-        const std::string key = entry_key(job.coef, job.k, job.r, options_from_env());
-        if (!R.entries.count(key)) {
-            if (R.entries.size() >= kAutoMaxKernels) return hipErrorNotSupported;
-            if (R.seen.size() > 4 * kAutoMaxKernels) R.seen.clear();
-            if (++R.seen[key] < kAutoMinUses) return hipErrorNotSupported;
-            R.seen.erase(key);
-        }
+    if (!eligible(a, mode)) return hipErrorNotSupported;
+    const unsigned k = a.k, r = a.r;
+    // the r x k matrix, contiguous
+    uint8_t buf[kJitMaxCoef];
+    const uint8_t* coef = a.coef;
+    if (a.coef_stride != k) {
+        for (unsigned i = 0; i < r; ++i) std::memcpy(buf + size_t(i) * k, a.coef + size_t(i) * a.coef_stride, k);
+        coef = buf;
     }
-    Entry* e = get_entry(job.coef, job.k, job.r, mode == kJitForce, lk);
-    if (e->state == 0) {
-        if (mode != kJitForce) return hipErrorNotReady;
-        R.cv.wait(lk, [&] { return e->state != 0; });
-    }
-    if (e->state != 1) return hipErrorNotSupported;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
-    auto it = e->dev.find(dev);
-    if (it == e->dev.end()) {
-        Loaded L;
-        hipError_t er = hipModuleLoadData(&L.mod, e->code.data());
-        if (er == hipSuccess) er = hipModuleGetFunction(&L.fn, L.mod, e->name.c_str());
-        if (er != hipSuccess) {
-            (void)hipGetLastError();
-            e->state = 2;
-            R.last_error = std::string("loading ") + e->name + ": " + hipGetErrorString(er);
-            return hipErrorNotSupported;
+    const Config* cfg = &config();
+    const Hit* hit = nullptr;
+    for (const Hit& h : t_hits)
+        if (h.name && h.cfg == cfg && h.dev == dev && h.k == k && h.r == r && !memcmp(h.coef.data(), coef, size_t(k) * r)) {
+            hit = &h;
+            break;
         }
-        int nb = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.fn, static_cast<int>(e->threads), 0) ==
-                hipSuccess &&
-            nb > 0)
-            L.blocks_per_cu = nb;
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
-            L.num_cu = ncu;
-        it = e->dev.emplace(dev, L).first;
+    Loaded L;
+    const char* name;
+    unsigned threads, upb;
+    if (hit) {
+        L = hit->L;
+        name = hit->name;
+        threads = hit->threads;
+        upb = hit->upb;
+    } else {
+        Registry& R = reg();
+        std::unique_lock<std::mutex> lk(R.mu);
+        if (mode == kJitAuto) {
+            const std::string key = entry_key(coef, k, r, options_for(k));
+            if (!R.entries.count(key)) {
+                if (R.entries.size() >= kAutoMaxKernels) return hipErrorNotSupported;
+                if (R.seen.size() > 4 * kAutoMaxKernels) R.seen.clear();
+                if (++R.seen[key] < kAutoMinUses) return hipErrorNotSupported;
+                R.seen.erase(key);
+            }
+        }
+        Entry* e = get_entry(coef, k, r, mode == kJitForce, lk);
+        if (e->state == 0) {
+            if (mode != kJitForce) return hipErrorNotReady;
+            R.cv.wait(lk, [&] { return e->state != 0; });
+        }
+        if (e->state != 1) return hipErrorNotSupported;
+        auto it = e->dev.find(dev);
+        if (it == e->dev.end()) {
+            Loaded nl;
+            hipError_t er = hipModuleLoadData(&nl.mod, e->code.data());
+            if (er == hipSuccess) er = hipModuleGetFunction(&nl.fn, nl.mod, e->name.c_str());
+            if (er != hipSuccess) {
+                (void)hipGetLastError();
+                e->state = 2;
+                R.last_error = std::string("loading ") + e->name + ": " + hipGetErrorString(er);
+                return hipErrorNotSupported;
+            }
+            int nb = 0;
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nl.fn, static_cast<int>(e->threads), 0) ==
+                    hipSuccess &&
+                nb > 0)
+                nl.blocks_per_cu = nb;
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+                nl.num_cu = ncu;
+            it = e->dev.emplace(dev, nl).first;
+        }
+        L = it->second;
+        name = e->name.c_str();  // stable: entries are never removed
+        threads = e->threads;
+        upb = e->units_per_block;
+        lk.unlock();
+        Hit& h = t_hits[t_hit_next++ % kHits];
+        h.cfg = cfg;
+        h.dev = dev;
+        h.k = k;
+        h.r = r;
+        h.coef.assign(coef, coef + size_t(k) * r);
+        h.L = L;
+        h.name = name;
+        h.threads = threads;
+        h.upb = upb;
     }
-    const Loaded L = it->second;
-    const char* name = e->name.c_str();  // stable: entries are never removed
-    const unsigned threads = e->threads, upb = e->units_per_block;
-    lk.unlock();
 
-    const uint64_t cps = (job.sz + kBsChunk - 1) / kBsChunk;
-    const uint64_t waves = cps * job.nstripes;
+    const uint64_t cps = (a.sz + kBsChunk - 1) / kBsChunk;
+    const uint64_t waves = cps * a.nstripes;
     if (waves >= (1ull << 32) - (1ull << 24)) return hipErrorNotSupported;
     const uint64_t need = (waves + upb - 1) / upb;
     const uint64_t cap = uint64_t(L.num_cu) * L.blocks_per_cu * 64;
     const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
     const uint64_t gwaves = uint64_t(grid) * upb;  // units per grid-stride step
     // struct Args of the generated source: 3 x u64, 4 x u32, k + r pointers
-    std::vector<uint64_t> args(5 + job.k + job.r);
-    args[0] = job.sz;
-    args[1] = job.in_sstride;
-    args[2] = job.out_sstride;
-    const uint32_t a32[4] = {job.nstripes, static_cast<uint32_t>(cps), static_cast<uint32_t>(gwaves % cps),
-                             static_cast<uint32_t>(gwaves / cps)};
+    uint64_t args[5 + kMaxWideIn + kMaxOut];
+    args[0] = a.sz;
+    args[1] = a.in_sstride;
+    args[2] = a.out_sstride;
+    const uint32_t a32[4] = {static_cast<uint32_t>(a.nstripes), static_cast<uint32_t>(cps),
+                             static_cast<uint32_t>(gwaves % cps), static_cast<uint32_t>(gwaves / cps)};
     std::memcpy(&args[3], a32, sizeof a32);
-    for (unsigned j = 0; j < job.k; ++j) args[5 + j] = reinterpret_cast<uint64_t>(job.in[j]);
-    for (unsigned i = 0; i < job.r; ++i) args[5 + job.k + i] = reinterpret_cast<uint64_t>(job.out[i]);
-    size_t size = args.size() * sizeof(uint64_t);
-    void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
-                      HIP_LAUNCH_PARAM_END};
-    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, 0, stream, nullptr, config);
+    for (unsigned j = 0; j < k; ++j) args[5 + j] = reinterpret_cast<uint64_t>(a.in[j]);
+    for (unsigned i = 0; i < r; ++i) args[5 + k + i] = reinterpret_cast<uint64_t>(a.out[i]);
+    size_t size = (5 + k + r) * sizeof(uint64_t);
+    void* conf[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, 0, stream, nullptr, conf);
     if (er == hipSuccess && name_out) *name_out = name;
     return er;
 }

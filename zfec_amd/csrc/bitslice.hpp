@@ -40,7 +40,15 @@ struct BsOptions {
     bool argload = true;             // block pointers loaded where used (no up-front SGPR spill)
     bool shift64 = true;             // bit transposes shift register pairs with 64-bit shifts (4-9 % fewer
                                      // VALU; cfg4 decode 380 -> 375 us, encode unchanged: profiles/r02_jit_shift64.log)
+    unsigned probe = 0;              // measurement variants (tools/jit_probe.py; results NOT the code's):
+                                     // 1 = no HBM traffic (inputs synthesised, stores dropped),
+                                     // 2 = no arithmetic (same loads and stores, outputs = XOR of raw inputs)
 };
+
+// Largest matrix (k * r coefficients per launch) the generator specialises:
+// the kernel's code grows with it (~10 instructions per coefficient), and so
+// does its compile time; larger launches run on matapply_bsg.
+constexpr unsigned kJitMaxCoef = 1600;
 
 // Row tiles of an r-row matrix, and whether they go to the waves of one
 // workgroup (2-8 tiles) or each wave walks all of them.
@@ -62,10 +70,10 @@ void set_jit_mode(JitMode m);
 // 0 on success, else -1 (jit_last_error() says why).
 int jit_prepare(const uint8_t* coef, unsigned k, unsigned r);
 
-// Launch the specialised kernel for job (job.coef holds the r x k matrix).
-// hipErrorNotSupported: not used for this launch (caller uses the table kernels);
+// Launch the specialised kernel for the matrix application `a`.
+// hipErrorNotSupported: not used for this launch (caller uses the other kernels);
 // hipErrorNotReady: not compiled yet (a background compile is queued).
-hipError_t launch_matapply_jit(const MatJob& job, hipStream_t stream, const char** name_out);
+hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const char** name_out);
 
 // Block until every queued compile has finished; returns the number of
 // specialised kernels compiled so far (failures excluded).

@@ -10,11 +10,16 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <memory>
 #include <new>
 #include <stdexcept>
@@ -29,6 +34,7 @@
 
 #include "../../include/zfec_hip.h"
 #include "bitslice.hpp"
+#include "config.hpp"
 #include "gf256.hpp"
 #include "host_pool.hpp"
 #include "kernels.hpp"
@@ -81,14 +87,10 @@ bool valid_code(const fec_t* c) { return c && c->enc_matrix && c->magic == magic
 
 // ---- per-thread, per-device staging -----------------------------------------
 
-constexpr int kSlots = 3;  // pipeline depth of the host path (H2D | kernel | D2H)
 constexpr int kStageSlots = 3;  // staged host path: copy-in | kernel | copy-out
 
 struct DevCtx {
     hipStream_t stream = nullptr;  // library stream: kernels of the host path, sync calls
-    hipStream_t h2d = nullptr;     // host -> device copies of the pipeline
-    hipStream_t d2h = nullptr;     // device -> host copies of the pipeline
-    hipEvent_t ev_in[kSlots] = {}, ev_cmp[kSlots] = {}, ev_out[kSlots] = {}, ev_start = nullptr;
     void* dbuf = nullptr;
     size_t dcap = 0;
     void* hbuf = nullptr;  // pinned
@@ -112,14 +114,6 @@ struct ThreadCtx {
             if (hipSetDevice(kv.first) != hipSuccess) continue;
             DevCtx& d = kv.second;
             if (d.stream) (void)hipStreamDestroy(d.stream);
-            if (d.h2d) (void)hipStreamDestroy(d.h2d);
-            if (d.d2h) (void)hipStreamDestroy(d.d2h);
-            for (int i = 0; i < kSlots; ++i) {
-                if (d.ev_in[i]) (void)hipEventDestroy(d.ev_in[i]);
-                if (d.ev_cmp[i]) (void)hipEventDestroy(d.ev_cmp[i]);
-                if (d.ev_out[i]) (void)hipEventDestroy(d.ev_out[i]);
-            }
-            if (d.ev_start) (void)hipEventDestroy(d.ev_start);
             for (int i = 0; i < kStageSlots; ++i)
                 if (d.ev_stg[i]) (void)hipEventDestroy(d.ev_stg[i]);
             if (d.dbuf) (void)hipFree(d.dbuf);
@@ -140,22 +134,6 @@ int dev_ctx(int device, DevCtx** out) {
         if (e != hipSuccess) return hip_fail(e, "hipStreamCreateWithFlags");
     }
     *out = &d;
-    return FEC_OK;
-}
-
-// Streams and events of the host-path pipeline, created on first use.
-int pipeline_ctx(DevCtx& d) {
-    if (d.h2d) return FEC_OK;
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&d.h2d, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&d.d2h, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&d.ev_start, hipEventDisableTiming)) != hipSuccess)
-        return hip_fail(e, "pipeline streams");
-    for (int i = 0; i < kSlots; ++i)
-        if ((e = hipEventCreateWithFlags(&d.ev_in[i], hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&d.ev_cmp[i], hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&d.ev_out[i], hipEventDisableTiming)) != hipSuccess)
-            return hip_fail(e, "pipeline events");
     return FEC_OK;
 }
 
@@ -230,11 +208,7 @@ int gpu_available() {
 // The stream is queried every 1024 spins, so an error ends the wait; past
 // 200 us it blocks in hipStreamSynchronize.  ZFEC_HIP_WAIT=sync turns it off.
 uint32_t* signal_slot(DevCtx& d) {
-    static const bool on = [] {
-        const char* e = getenv("ZFEC_HIP_WAIT");
-        return !(e && !strcmp(e, "sync"));
-    }();
-    if (!on) return nullptr;
+    if (!config().wait_signal) return nullptr;
     if (!d.flag) {
         void* p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess) {
@@ -286,74 +260,82 @@ struct DeviceGuard {
 constexpr size_t align_up_4k(size_t x) { return (x + 4095) / 4096 * 4096; }
 
 // in[j] / out[i] are device pointers (block bases of stripe 0); stripes are
-// in_sstride / out_sstride apart.  Splits into launches that respect the
-// kernel's limits: <= kMaxIn inputs (later input groups XOR-accumulate),
-// <= kMaxOut outputs and <= kMaxCoef coefficients per launch, and at most
-// launch_units() kMinChunk-byte units per launch.  Blocks longer than that
-// are cut into byte ranges of their own launches: output byte x depends only
-// on byte x of the inputs (zfec/fec.c:494-503, :547-556).
-size_t launch_units() {
-    // ZFEC_HIP_LAUNCH_UNITS lowers the limit so tests reach the split paths
-    // with small buffers; the kernels' own bound is < 2^32 units per launch.
-    static const size_t units = [] {
-        const char* v = getenv("ZFEC_HIP_LAUNCH_UNITS");
-        const unsigned long long u = v && *v ? strtoull(v, nullptr, 10) : 0;
-        return u >= 1024 && u < (1ull << 31) ? static_cast<size_t>(u) : size_t(1) << 31;
-    }();
-    return units;
-}
+// in_sstride / out_sstride apart; coef is r x k with rows coef_stride apart.
+// Splits into launches that respect the kernels' limits: <= kMaxOut outputs
+// per launch; all k inputs in one pass where a bit-sliced kernel takes them
+// (wide_launch_ok), otherwise groups of <= kMaxIn inputs, later groups
+// XOR-accumulating, and <= kMaxCoef coefficients per launch; at most
+// Config::launch_units kMinChunk-byte units per launch.  Blocks longer than
+// that are cut into byte ranges of their own launches: output byte x depends
+// only on byte x of the inputs (zfec/fec.c:494-503, :547-556).
+thread_local unsigned t_launches = 0;  // launches made by this thread (the signal path checks it made one)
+thread_local int t_last_wait = 0;      // 1: the last synchronous small call waited on its kernel's signal (fec_last_wait)
 
-int apply_matrix_range(const uint8_t* coef, unsigned k, unsigned r, const uint8_t* const* in, uint8_t* const* out,
-                       size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride, hipStream_t stream);
+int apply_matrix_range(const uint8_t* coef, unsigned coef_stride, unsigned k, unsigned r, const uint8_t* const* in,
+                       uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
+                       hipStream_t stream);
 
 int apply_matrix(const uint8_t* coef /* r x k */, unsigned k, unsigned r, const uint8_t* const* in,
                  uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
-                 hipStream_t stream) {
+                 hipStream_t stream, unsigned coef_stride = 0) {
     if (r == 0 || sz == 0 || nstripes == 0) return FEC_OK;
+    if (!coef_stride) coef_stride = k;
     const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
-    const size_t max_units = launch_units();
-    if (cps <= max_units) return apply_matrix_range(coef, k, r, in, out, sz, nstripes, in_sstride, out_sstride, stream);
+    const size_t max_units = config().launch_units;
+    if (cps <= max_units)
+        return apply_matrix_range(coef, coef_stride, k, r, in, out, sz, nstripes, in_sstride, out_sstride, stream);
     // near-equal byte ranges on 4 KiB boundaries, each within the unit limit
     const size_t pieces = (cps + max_units - 1) / max_units;
     const size_t piece = align_up_4k((sz + pieces - 1) / pieces);
-    std::vector<const uint8_t*> pin(k);
-    std::vector<uint8_t*> pout(r);
+    const uint8_t* pin[kMaxWideIn];
+    uint8_t* pout[kMaxWideIn];
     for (size_t b0 = 0; b0 < sz; b0 += piece) {
         const size_t len = std::min(piece, sz - b0);
         for (unsigned j = 0; j < k; ++j) pin[j] = in[j] + b0;
         for (unsigned i = 0; i < r; ++i) pout[i] = out[i] + b0;
-        if (apply_matrix_range(coef, k, r, pin.data(), pout.data(), len, nstripes, in_sstride, out_sstride, stream))
+        if (apply_matrix_range(coef, coef_stride, k, r, pin, pout, len, nstripes, in_sstride, out_sstride, stream))
             return t_status;
     }
     return FEC_OK;
 }
 
-int apply_matrix_range(const uint8_t* coef, unsigned k, unsigned r, const uint8_t* const* in, uint8_t* const* out,
-                       size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride, hipStream_t stream) {
+int apply_matrix_range(const uint8_t* coef, unsigned coef_stride, unsigned k, unsigned r, const uint8_t* const* in,
+                       uint8_t* const* out, size_t sz, size_t nstripes, size_t in_sstride, size_t out_sstride,
+                       hipStream_t stream) {
     const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
-    const size_t stripes_per_launch = std::max<size_t>(1, launch_units() / cps);
-    for (unsigned j0 = 0; j0 < k; j0 += kMaxIn) {
-        const unsigned kg = std::min<unsigned>(kMaxIn, k - j0);
-        const unsigned rmax = std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
-        for (unsigned i0 = 0; i0 < r; i0 += rmax) {
-            const unsigned rg = std::min<unsigned>(rmax, r - i0);
+    const size_t stripes_per_launch = std::max<size_t>(1, config().launch_units / cps);
+    // wide codes: every input in one bit-sliced pass per row group
+    const bool wide = k > static_cast<unsigned>(kMaxIn) && wide_launch_ok(k, std::min<unsigned>(r, kMaxOut), sz);
+    const unsigned kstep = wide ? k : static_cast<unsigned>(kMaxIn);
+    const uint8_t* pin[kMaxWideIn];
+    uint8_t* pout[kMaxWideIn];
+    for (unsigned j0 = 0; j0 < k; j0 += kstep) {
+        const unsigned kg = std::min<unsigned>(kstep, k - j0);
+        const unsigned rmax = wide ? static_cast<unsigned>(kMaxOut)
+                                   : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
+        const unsigned ngroups = (r + rmax - 1) / rmax;
+        for (unsigned g = 0; g < ngroups; ++g) {
+            // near-equal row groups
+            const unsigned i0 = g * r / ngroups, rg = (g + 1) * r / ngroups - i0;
             for (size_t s0 = 0; s0 < nstripes; s0 += stripes_per_launch) {
                 const size_t ns = std::min(stripes_per_launch, nstripes - s0);
-                MatJob job;
-                std::memset(&job, 0, sizeof job);
-                job.sz = sz;
-                job.in_sstride = in_sstride;
-                job.out_sstride = out_sstride;
-                job.nstripes = static_cast<uint32_t>(ns);
-                job.k = kg;
-                job.r = rg;
-                job.accumulate = j0 > 0;
-                for (unsigned j = 0; j < kg; ++j) job.in[j] = in[j0 + j] + s0 * in_sstride;
-                for (unsigned i = 0; i < rg; ++i) job.out[i] = out[i0 + i] + s0 * out_sstride;
-                for (unsigned i = 0; i < rg; ++i)
-                    for (unsigned j = 0; j < kg; ++j) job.coef[i * kg + j] = coef[size_t(i0 + i) * k + j0 + j];
-                hipError_t e = launch_matapply(job, stream);
-                if (e != hipSuccess) return hip_fail(e, "launch_matapply");
+                for (unsigned j = 0; j < kg; ++j) pin[j] = in[j0 + j] + s0 * in_sstride;
+                for (unsigned i = 0; i < rg; ++i) pout[i] = out[i0 + i] + s0 * out_sstride;
+                ApplySpec a;
+                a.coef = coef + size_t(i0) * coef_stride + j0;
+                a.coef_stride = coef_stride;
+                a.k = kg;
+                a.r = rg;
+                a.in = pin;
+                a.out = pout;
+                a.sz = sz;
+                a.nstripes = ns;
+                a.in_sstride = in_sstride;
+                a.out_sstride = out_sstride;
+                a.accumulate = j0 > 0;
+                ++t_launches;
+                const hipError_t e = launch_apply(a, stream);
+                if (e != hipSuccess) return hip_fail(e, "launch_apply");
             }
         }
     }
@@ -376,6 +358,7 @@ struct Marshal {
 int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marshal& m) {
     m.in_host.clear();
     m.out_host.clear();
+    m.all_pinned = true;
     m.zin.assign(in, in + nin);
     m.zout.assign(out, out + nout);
     int dev = -1;
@@ -409,94 +392,30 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
     return FEC_OK;
 }
 
-// Host blocks of up to this many bytes in total go through one pinned bounce
-// buffer (one H2D / D2H each way); larger ones stream through the pipeline.
-// From kStageMin bytes, blocks of at least kStageMinBlock bytes take the
-// staged path too: its overlapped copy-in / kernel / copy-out beats the bounce
+// Host blocks of up to Config::pack_limit bytes in total (4 MiB) go through
+// one pinned bounce buffer (one H2D / D2H each way); larger ones take the
+// staged path.  From Config::stage_min bytes (512 KiB), blocks of at least
+// kStageMinBlock bytes take the staged path too: its overlapped copy-in / kernel / copy-out beats the bounce
 // buffer's serial memcpy / DMA / kernel / DMA / memcpy (K=3/M=10 from bytes,
 // 1 MiB stripe: 137 vs 209 us per encode; 256 KiB stripe: 69 vs 77 us), but
 // not for many small blocks (K=20/M=60, 256 KiB stripe of 13 KB blocks: 260
 // vs 122 us; tools/host_lat_ab.py, profiles/r02_host_lat_ab.log).
-// (ZFEC_HIP_PACK_LIMIT / ZFEC_HIP_STAGE_MIN override, read per call for A/B runs.)
-size_t env_size(const char* name, size_t dflt) {
-    const char* e = getenv(name);
-    return e && *e ? static_cast<size_t>(strtoull(e, nullptr, 10)) : dflt;
-}
-size_t pack_limit() { return env_size("ZFEC_HIP_PACK_LIMIT", size_t(4) << 20); }
-size_t stage_min() { return env_size("ZFEC_HIP_STAGE_MIN", size_t(512) << 10); }
 constexpr size_t kStageMinBlock = size_t(64) << 10;
 // Up to this many bytes the kernel accesses the bounce buffer in place.
 constexpr size_t kZeroCopyLimit = size_t(256) << 10;
-// Bytes of each block per pipeline chunk.
-constexpr size_t kPipeChunk = size_t(2) << 20;
-// Small calls: from this many bytes per direction the bounce-buffer copies run
-// on the host pool (ZFEC_HIP_POOL_COPY_MIN, read per call for A/B runs).  Off by
-// default: waking the pool costs more than it saves below 4 MiB (1 MiB
-// K=3/M=10 stripe: 255 us pooled vs 209 us on the calling thread,
-// profiles/r02_host_lat_ab.log).
-size_t pool_copy_min() {
-    const char* e = getenv("ZFEC_HIP_POOL_COPY_MIN");
-    return e && *e ? static_cast<size_t>(strtoull(e, nullptr, 10)) : SIZE_MAX;
-}
+// Small calls: from Config::pool_copy_min bytes per direction the
+// bounce-buffer copies run on the host pool.  Off by default: waking the pool
+// costs more than it saves below 4 MiB (1 MiB K=3/M=10 stripe: 255 us pooled
+// vs 209 us on the calling thread, profiles/r02_host_lat_ab.log).
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Fault in fresh host pages before they are page-locked: a fresh output
-// `bytes` object's pages are not mapped yet, and hipHostRegister faulted them
-// in one by one (K=3/M=10, 64 MiB: 12.8 ms for 156 MB of outputs,
-// profiles/r01_host_breakdown.log).  MADV_POPULATE_WRITE over the ranges from
-// 4 threads maps them at ~45 GB/s on the MI355X host with transparent huge
-// pages (tools/fault_probe.c, profiles/r02_fault_probe.log); where the kernel
-// lacks it (EINVAL, before Linux 5.14) each page is written once instead.
-// The ranges' contents are unspecified afterwards (they are outputs).
-void populate_parallel(const std::vector<std::pair<uintptr_t, uintptr_t>>& ranges) {
-    static const uintptr_t page = [] {
-        const long v = sysconf(_SC_PAGESIZE);
-        return static_cast<uintptr_t>(v > 0 ? v : 4096);
-    }();
-    constexpr int kThreads = 4;
-    constexpr int kPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
-    size_t total = 0;
-    for (const auto& rg : ranges) total += rg.second - rg.first;
-    if (total < (size_t(8) << 20)) return;  // small: not worth the threads
-    // cut the ranges into kThreads page-aligned pieces of near-equal size
-    std::vector<std::vector<std::pair<uintptr_t, uintptr_t>>> parts(kThreads);
-    const size_t share = (total + kThreads - 1) / kThreads;
-    size_t acc = 0;
-    for (const auto& rg : ranges) {
-        uintptr_t a = (rg.first + page - 1) / page * page;
-        const uintptr_t e = rg.second / page * page;
-        while (a < e) {
-            const int t = static_cast<int>(std::min<size_t>(acc / share, kThreads - 1));
-            const size_t room = (size_t(t) + 1) * share - acc;
-            const uintptr_t b = std::min<uintptr_t>(e, (a + std::max<size_t>(room, page) + page - 1) / page * page);
-            parts[t].emplace_back(a, b);
-            acc += b - a;
-            a = b;
-        }
-    }
-    auto work = [](const std::vector<std::pair<uintptr_t, uintptr_t>>& pr) {
-        for (const auto& rg : pr) {
-            if (madvise(reinterpret_cast<void*>(rg.first), rg.second - rg.first, kPopulateWrite) == 0) continue;
-            for (uintptr_t q = rg.first; q < rg.second; q += page) *reinterpret_cast<volatile char*>(q) = 0;
-        }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < kThreads; ++t)
-        if (!parts[t].empty()) th.emplace_back(work, std::cref(parts[t]));
-    work(parts[0]);
-    for (auto& x : th) x.join();
-}
-
-// Pins pageable host ranges for the duration of one call (RAII), so the
-// pipeline can DMA them in place; ZFEC_HIP_REGISTER=0 disables it (the copies
-// then go through HIP's own staging of pageable memory).
 // ZFEC_HIP_TRACE_HOST=1: per-phase times of a large pageable call on stderr.
 struct HostTrace {
     bool on;
     std::chrono::steady_clock::time_point t;
     std::string line;
-    HostTrace() : on(getenv("ZFEC_HIP_TRACE_HOST") != nullptr), t(std::chrono::steady_clock::now()) {}
+    HostTrace() : on(config().trace_host), t(std::chrono::steady_clock::now()) {}
     // accumulated waits inside a loop: lap() starts one, add(i) ends it into slot i
     std::chrono::steady_clock::time_point l;
     double acc[3] = {0, 0, 0};
@@ -525,44 +444,6 @@ struct HostTrace {
     }
 };
 
-struct HostPins {
-    std::vector<void*> pinned;
-    ~HostPins() { release(); }
-    void release() {
-        for (void* p : pinned) (void)hipHostUnregister(p);
-        pinned.clear();
-    }
-    // Page-lock every range [p, p + n) (merged where they share pages, since a
-    // page can be registered once) for the duration of the call.
-    bool pin_all(std::vector<std::pair<uintptr_t, uintptr_t>> ranges) {
-        static const uintptr_t page = [] {
-            const long v = sysconf(_SC_PAGESIZE);
-            return static_cast<uintptr_t>(v > 0 ? v : 4096);
-        }();
-        for (auto& rg : ranges) {
-            rg.first = rg.first / page * page;
-            rg.second = (rg.second + page - 1) / page * page;
-        }
-        std::sort(ranges.begin(), ranges.end());
-        std::vector<std::pair<uintptr_t, uintptr_t>> merged;
-        for (const auto& rg : ranges) {
-            if (!merged.empty() && rg.first <= merged.back().second)
-                merged.back().second = std::max(merged.back().second, rg.second);
-            else
-                merged.push_back(rg);
-        }
-        for (const auto& rg : merged) {
-            void* q = reinterpret_cast<void*>(rg.first);
-            if (hipHostRegister(q, rg.second - rg.first, hipHostRegisterMapped) != hipSuccess) {
-                (void)hipGetLastError();
-                return false;
-            }
-            pinned.push_back(q);
-        }
-        return true;
-    }
-};
-
 // Kernel-visible address of the host block [p, p + n), or nullptr unless the
 // whole block is page-locked (first and last byte mapped at the same offset).
 const uint8_t* mapped_block(const void* p, size_t n) {
@@ -575,238 +456,6 @@ const uint8_t* mapped_block(const void* p, size_t n) {
     return static_cast<const uint8_t*>(da);
 }
 
-// ZFEC_HIP_POPULATE=1 turns on the parallel pre-faulting of fresh outputs
-// before they are locked (A/B runs; read per call)
-bool populate_enabled() {
-    const char* e = getenv("ZFEC_HIP_POPULATE");
-    return e && e[0] == '1';
-}
-
-bool register_pageable() {
-    static const bool on = [] {
-        const char* e = getenv("ZFEC_HIP_REGISTER");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-constexpr int FEC_EAGAIN_INTERNAL = -1;  // a page could not be locked: take another path
-
-size_t pageable_chunk() {
-    const char* e = getenv("ZFEC_HIP_PAGEABLE_CHUNK");  // bytes per block per chunk (A/B runs)
-    const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0;
-    return v >= (64u << 10) ? static_cast<size_t>(v) : size_t(4) << 20;
-}
-
-// Page-locks the host blocks of a call chunk by chunk: lock(off, len) locks
-// bytes [off, off + len) of every listed host block (whole pages; a page two
-// blocks share, or one locked by an earlier chunk, is locked once).  `fresh`
-// blocks (new outputs) may first be faulted in from several threads.  Every
-// lock is released by release() / the destructor.
-struct PageLocker {
-    std::vector<const void*> blocks;
-    std::vector<char> fresh;
-    bool populate = false;
-    HostPins pins;
-    std::map<uintptr_t, uintptr_t> locked;  // disjoint locked page ranges, start -> end (adjacent ones merged)
-
-    // the parts of [a, e) not locked yet
-    std::vector<std::pair<uintptr_t, uintptr_t>> unlocked_parts(uintptr_t a, uintptr_t e) const {
-        std::vector<std::pair<uintptr_t, uintptr_t>> parts;
-        auto it = locked.upper_bound(a);
-        if (it != locked.begin() && std::prev(it)->second > a) --it;
-        uintptr_t x = a;
-        for (; it != locked.end() && it->first < e && x < e; ++it) {
-            if (it->first > x) parts.emplace_back(x, it->first);
-            x = std::max(x, it->second);
-        }
-        if (x < e) parts.emplace_back(x, e);
-        return parts;
-    }
-
-    void mark(uintptr_t a, uintptr_t e) {
-        auto it = locked.emplace(a, e).first;
-        auto nx = std::next(it);
-        if (nx != locked.end() && nx->first == e) {  // merge with the range after
-            it->second = nx->second;
-            locked.erase(nx);
-        }
-        if (it != locked.begin()) {  // and with the one before
-            auto pv = std::prev(it);
-            if (pv->second == it->first) {
-                pv->second = it->second;
-                locked.erase(it);
-            }
-        }
-    }
-
-    bool lock(size_t off, size_t len) {
-        static const uintptr_t page = [] {
-            const long v = sysconf(_SC_PAGESIZE);
-            return static_cast<uintptr_t>(v > 0 ? v : 4096);
-        }();
-        std::vector<std::pair<uintptr_t, uintptr_t>> todo, pop;
-        for (size_t b = 0; b < blocks.size(); ++b) {
-            const uintptr_t a = reinterpret_cast<uintptr_t>(blocks[b]) + off;
-            for (const auto& q : unlocked_parts(a / page * page, (a + len + page - 1) / page * page)) {
-                todo.push_back(q);
-                mark(q.first, q.second);
-                if (fresh[b] && populate) pop.push_back(q);
-            }
-        }
-        if (!pop.empty()) populate_parallel(pop);
-        for (const auto& q : todo) {
-            void* p = reinterpret_cast<void*>(q.first);
-            if (hipHostRegister(p, q.second - q.first, hipHostRegisterMapped) != hipSuccess) {
-                (void)hipGetLastError();
-                return false;
-            }
-            pins.pinned.push_back(p);
-        }
-        return true;
-    }
-    void release() { pins.release(); }
-};
-
-// Large host-memory call: the byte range is cut into chunks of kPipeChunk;
-// chunk c's inputs go H2D on d.h2d, its kernel runs on d.stream, its outputs
-// go D2H on d.d2h, with kSlots device staging slots in flight, so copies in
-// both directions overlap each other and the kernels.  Device-resident blocks
-// are read / written in place.
-int run_pipeline(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out,
-                 size_t sz, Marshal& m, hipStream_t user) {
-    if (pipeline_ctx(d)) return t_status;
-    const size_t C = kPipeChunk;
-    const size_t nin = m.in_host.size(), nout = m.out_host.size();
-    const size_t slot_bytes = C * (nin + nout);
-    if (ensure_dbuf(d, slot_bytes * kSlots)) return t_status;
-    hipError_t e;
-    // order after the caller's prior work on `user` (device inputs may be produced there)
-    if ((e = hipEventRecord(d.ev_start, user)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    if ((e = hipStreamWaitEvent(d.h2d, d.ev_start, 0)) != hipSuccess ||
-        (e = hipStreamWaitEvent(d.stream, d.ev_start, 0)) != hipSuccess)
-        return hip_fail(e, "hipStreamWaitEvent");
-    std::vector<const uint8_t*> cin(k);
-    std::vector<uint8_t*> cout(r);
-    const size_t nchunks = (sz + C - 1) / C;
-    for (size_t c = 0; c < nchunks; ++c) {
-        const int s = static_cast<int>(c % kSlots);
-        const size_t off = c * C, len = std::min(C, sz - off);
-        uint8_t* base = static_cast<uint8_t*>(d.dbuf) + s * slot_bytes;
-        if (c >= static_cast<size_t>(kSlots)) {  // slot reuse: its previous outputs have left
-            if ((e = hipStreamWaitEvent(d.h2d, d.ev_out[s], 0)) != hipSuccess) return hip_fail(e, "wait");
-            if ((e = hipStreamWaitEvent(d.stream, d.ev_out[s], 0)) != hipSuccess) return hip_fail(e, "wait");
-        }
-        for (unsigned j = 0; j < k; ++j) cin[j] = in[j] + off;
-        for (unsigned i = 0; i < r; ++i) cout[i] = out[i] + off;
-        for (size_t q = 0; q < nin; ++q) {
-            uint8_t* dst = base + q * C;
-            if ((e = hipMemcpyAsync(dst, in[m.in_host[q]] + off, len, hipMemcpyHostToDevice, d.h2d)) != hipSuccess)
-                return hip_fail(e, "hipMemcpyAsync H2D");
-            cin[m.in_host[q]] = dst;
-        }
-        for (size_t q = 0; q < nout; ++q) cout[m.out_host[q]] = base + (nin + q) * C;
-        if ((e = hipEventRecord(d.ev_in[s], d.h2d)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-        if ((e = hipStreamWaitEvent(d.stream, d.ev_in[s], 0)) != hipSuccess) return hip_fail(e, "wait");
-        if (apply_matrix(coef, k, r, cin.data(), cout.data(), len, 1, 0, 0, d.stream)) return t_status;
-        if ((e = hipEventRecord(d.ev_cmp[s], d.stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-        if ((e = hipStreamWaitEvent(d.d2h, d.ev_cmp[s], 0)) != hipSuccess) return hip_fail(e, "wait");
-        for (size_t q = 0; q < nout; ++q)
-            if ((e = hipMemcpyAsync(out[m.out_host[q]] + off, base + (nin + q) * C, len, hipMemcpyDeviceToHost,
-                                    d.d2h)) != hipSuccess)
-                return hip_fail(e, "hipMemcpyAsync D2H");
-        if ((e = hipEventRecord(d.ev_out[s], d.d2h)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    }
-    if ((e = hipStreamSynchronize(d.d2h)) != hipSuccess || (e = hipStreamSynchronize(d.stream)) != hipSuccess)
-        return hip_fail(e, "hipStreamSynchronize");
-    return set_status(FEC_OK);
-}
-
-// Large pageable host blocks, zero-copy: the blocks are page-locked chunk by
-// chunk (kPageableChunk bytes of every block), each chunk's kernel launched as
-// soon as its pages are locked, so the GPU's work (the kernel reads and writes
-// host memory over PCIe) on chunk c overlaps the host's faulting and locking
-// of chunk c + 1.  Fresh output pages (new `bytes` objects) are faulted in from
-// several threads first (populate_parallel), which locks them much faster
-// than hipHostRegister faulting them one by one.  Every lock is released after
-// the stream has drained.  FEC_EAGAIN_INTERNAL when a range cannot be locked
-// (nothing is left locked; the caller falls back to the copy pipeline, which
-// recomputes every output).
-int run_pageable(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out, size_t sz,
-                 Marshal& m, hipStream_t st, unsigned flags) {
-    HostTrace tr;
-    PageLocker lk;
-    lk.populate = !(flags & FEC_FLAG_NO_POPULATE) && populate_enabled();
-    // a block already page-locked by the caller is used as it is
-    std::vector<char> host_in(k, 0), host_out(r, 0);
-    std::vector<const uint8_t*> base_in(m.zin);  // kernel-visible bases of device / caller-locked blocks
-    std::vector<uint8_t*> base_out(m.zout);
-    for (int i : m.in_host) {
-        const uint8_t* z = mapped_block(in[i], sz);
-        if (z) base_in[i] = z;
-        else {
-            host_in[i] = 1;
-            lk.blocks.push_back(in[i]);
-            lk.fresh.push_back(0);
-        }
-    }
-    for (int i : m.out_host) {
-        const uint8_t* z = mapped_block(out[i], sz);
-        if (z) base_out[i] = const_cast<uint8_t*>(z);
-        else {
-            host_out[i] = 1;
-            lk.blocks.push_back(out[i]);
-            lk.fresh.push_back(1);
-        }
-    }
-    auto fail = [&]() {
-        (void)hipStreamSynchronize(st);  // chunks already launched read / write locked pages
-        lk.release();
-        return FEC_EAGAIN_INTERNAL;
-    };
-    std::vector<const uint8_t*> zin(k);
-    std::vector<uint8_t*> zout(r);
-    const size_t C = pageable_chunk();
-    tr.mark("classify");
-    for (size_t off = 0; off < sz; off += C) {
-        const size_t len = std::min(C, sz - off);
-        if (!lk.lock(off, len)) return fail();
-        tr.mark("lock");
-        for (unsigned j = 0; j < k; ++j) {
-            zin[j] = base_in[j] + off;
-            if (host_in[j] && !(zin[j] = mapped_block(in[j] + off, len))) return fail();
-        }
-        for (unsigned i = 0; i < r; ++i) {
-            zout[i] = base_out[i] + off;
-            if (host_out[i] && !(zout[i] = const_cast<uint8_t*>(mapped_block(out[i] + off, len)))) return fail();
-        }
-        if (apply_matrix(coef, k, r, zin.data(), zout.data(), len, 1, 0, 0, st)) {
-            const int e = t_status;
-            (void)hipStreamSynchronize(st);
-            return e;
-        }
-        tr.mark("launch");
-    }
-    const hipError_t e = hipStreamSynchronize(st);
-    tr.mark("sync");
-    lk.release();
-    tr.mark("unregister");
-    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    return set_status(FEC_OK);
-}
-
-// Host path for large pageable calls (ZFEC_HIP_HOST_PATH, read per call for
-// A/B runs): "stage" (run_staged), "lock" (run_pageable) or "copy"
-// (run_pipeline with HIP's own staging of pageable memory).
-enum class HostPath { kStage, kLock, kCopy };
-
-HostPath host_path() {
-    const char* e = getenv("ZFEC_HIP_HOST_PATH");
-    if (e && !strcmp(e, "lock")) return HostPath::kLock;
-    if (e && !strcmp(e, "copy")) return HostPath::kCopy;
-    return HostPath::kStage;
-}
-
 // Bytes of every host block per staged chunk: ZFEC_HIP_STAGE_CHUNK, else
 // at most a quarter of the block (so that copy-in, kernel and copy-out of
 // consecutive chunks overlap) and at most about 16 MiB of staging per chunk
@@ -814,9 +463,7 @@ HostPath host_path() {
 // (K=3/M=10, 64 MiB from bytes: 8 MiB chunks 8.7 GB/s encode, 16-20 MiB 9.3;
 // 2.5 MiB 6.4; profiles/r02_host_stage_ab.log).
 size_t staged_chunk(size_t nblocks, size_t sz) {
-    const char* e = getenv("ZFEC_HIP_STAGE_CHUNK");
-    const unsigned long long v = e && *e ? strtoull(e, nullptr, 10) : 0;
-    if (v >= (64u << 10)) return static_cast<size_t>(v) / 4096 * 4096;
+    if (const size_t v = config().stage_chunk) return v;
     const size_t total = size_t(16) << 20, g = size_t(64) << 10;
     const size_t by_total = total / std::max<size_t>(1, nblocks) / g * g;
     const size_t quarter = (sz + 4 * g - 1) / (4 * g) * g;  // at least 4 chunks, so the stages overlap
@@ -1106,12 +753,13 @@ int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, con
 
 // Run `coef` (r x k) over in -> out.  Device blocks are used in place; host
 // blocks are staged (small calls: one pinned bounce buffer each way; large
-// calls: the chunked pipeline).  Synchronous unless FEC_FLAG_ASYNC and every
+// calls: the staged path).  Synchronous unless FEC_FLAG_ASYNC and every
 // block is device memory.
 int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out, size_t sz,
                void* stream_arg, unsigned flags) {
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
-    Marshal m;
+    thread_local Marshal t_m;  // reused: no allocation per call once its vectors have grown
+    Marshal& m = t_m;
     if (flags & FEC_FLAG_HOST_MEMORY) {  // the caller vouches: every block is host memory
         for (unsigned j = 0; j < k; ++j)
             if (!in[j]) return set_status(FEC_EINVAL, "input block %u is NULL", j);
@@ -1119,6 +767,8 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
             if (!out[i]) return set_status(FEC_EINVAL, "output block %u is NULL", i);
         m.zin.assign(in, in + k);
         m.zout.assign(out, out + r);
+        m.in_host.clear();
+        m.out_host.clear();
         for (unsigned j = 0; j < k; ++j) m.in_host.push_back(static_cast<int>(j));
         for (unsigned i = 0; i < r; ++i) m.out_host.push_back(static_cast<int>(i));
         m.all_pinned = false;
@@ -1132,6 +782,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream_arg);
     if (sz == 0 || r == 0) return set_status(FEC_OK);
     const size_t nhost = m.in_host.size() + m.out_host.size();
+    const Config& cfg = config();
     hipError_t e;
     if (nhost == 0) {
         if (apply_matrix(coef, k, r, in, out, sz, 1, 0, 0, st)) return t_status;
@@ -1141,7 +792,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     }
     // Page-locked host blocks are read and written by the kernel itself over
     // PCIe (zero-copy): both link directions run at once with no staging
-    // copies (K=3/M=10, 64 MiB: 21 GB/s of input vs 16.6 through the chunked
+    // copies (K=3/M=10, 64 MiB: 21 GB/s of input vs 16.6 through a chunked
     // copy pipeline; tools/mb_host.hip).
     auto map_all = [&]() {
         bool ok = true;
@@ -1149,25 +800,15 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         for (int i : m.out_host) ok = ok && (m.zout[i] = const_cast<uint8_t*>(mapped_block(out[i], sz))) != nullptr;
         return ok;
     };
-    auto zero_copy = [&](bool async) -> int {
+    if (m.all_pinned && map_all()) {
         if (apply_matrix(coef, k, r, m.zin.data(), m.zout.data(), sz, 1, 0, 0, st)) return t_status;
-        if (!async && (e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+        if (!(flags & FEC_FLAG_ASYNC) && (e = hipStreamSynchronize(st)) != hipSuccess)
+            return hip_fail(e, "hipStreamSynchronize");
         return set_status(FEC_OK);
-    };
-    if (m.all_pinned && map_all()) return zero_copy((flags & FEC_FLAG_ASYNC) != 0);
-    if (sz * nhost > pack_limit() || (sz * nhost > stage_min() && sz >= kStageMinBlock)) {
-        // large pageable blocks: staged through pinned slots by the host
-        // threads (default), or page-locked for the call and accessed in place,
-        // with the chunked copy pipeline as the fallback when they cannot be
-        // mapped
-        const HostPath hp = host_path();
-        if (hp == HostPath::kStage) return run_staged(*d, coef, k, r, in, out, sz, m, st);
-        if (hp == HostPath::kLock && register_pageable()) {
-            const int st0 = run_pageable(coef, k, r, in, out, sz, m, st, flags);
-            if (st0 != FEC_EAGAIN_INTERNAL) return st0;
-        }
-        return run_pipeline(*d, coef, k, r, in, out, sz, m, st);
     }
+    // large pageable blocks: staged through pinned slots by the host threads
+    if (sz * nhost > cfg.pack_limit || (sz * nhost > cfg.stage_min && sz >= kStageMinBlock))
+        return run_staged(*d, coef, k, r, in, out, sz, m, st);
 
     // small call: pack the host inputs into the thread's pinned buffer.  Up to
     // kZeroCopyLimit bytes the kernel reads them and writes the host outputs
@@ -1181,9 +822,9 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     const size_t nin = m.in_host.size(), nout = m.out_host.size();
     if (ensure_hbuf(*d, slot * (nin + nout))) return t_status;
     uint8_t* hb = static_cast<uint8_t*>(d->hbuf);  // free: the previous call on this thread synchronised
-    // from pool_copy_min() bytes per direction the copies run on the host pool
-    // (256 KiB pieces), below it on this thread
-    const bool pooled = sz * std::max(nin, nout) >= pool_copy_min();
+    // from Config::pool_copy_min bytes per direction the copies run on the
+    // host pool (256 KiB pieces), below it on this thread
+    const bool pooled = sz * std::max(nin, nout) >= cfg.pool_copy_min;
     auto copy_blocks = [&](bool to_slot) {
         CopyLatch latch;
         const size_t n = to_slot ? nin : nout;
@@ -1205,8 +846,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // 40 us in the kernel over PCIe; tools/small_call_probe.py under
     // rocprofv3, profiles/r02_small_calls.log).  ZFEC_HIP_ZC_WIDE=1 keeps
     // them zero-copy (A/B runs).
-    const char* zcw = getenv("ZFEC_HIP_ZC_WIDE");
-    const bool zc_kernel = (k <= 4 && r <= 8) || (zcw && zcw[0] == '1');
+    const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide;
     bool signalled = false;
     if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
@@ -1216,8 +856,10 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         // signals its own completion
         if (k <= 4 && r <= 8 && sz <= 4096)
             if (uint32_t* f = signal_slot(*d)) matapply_request_signal(f, d->seq);
+        const unsigned launches0 = t_launches;
         const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st);
-        signalled = st0 == FEC_OK && matapply_signal_used();
+        // the kernel's signal covers the call only if it was its one launch
+        signalled = st0 == FEC_OK && matapply_signal_used() && t_launches - launches0 == 1;
         matapply_request_signal(nullptr, 0);  // an unconsumed request must not reach a later launch
         if (st0) return t_status;
     } else {
@@ -1232,6 +874,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
                                         st)) != hipSuccess)
             return hip_fail(e, "hipMemcpyAsync D2H");
     }
+    t_last_wait = signalled ? 1 : 0;
     if ((e = signalled ? wait_signal(*d, st) : hipStreamSynchronize(st)) != hipSuccess)
         return hip_fail(e, "hipStreamSynchronize");
     copy_blocks(false);
@@ -1246,15 +889,15 @@ int check_block_nums(const fec_t* code, const unsigned* nums, size_t num) {
     return FEC_OK;
 }
 
-// Rows of the decode matrix for the missing primaries (ascending), r x k.
-// The decode matrix rows to apply: the missing primaries' (ascending), or with
-// all_primaries every primary's (a present primary's row is a unit vector:
-// the output is a copy, so the k outputs are the stripe in order).
+// The decode matrix rows to apply (r x k, into `rows`): the missing
+// primaries' (ascending), or with all_primaries every primary's (a present
+// primary's row is a unit vector: the output is a copy, so the k outputs are
+// the stripe in order).
 int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& rows, unsigned& r,
                 bool all_primaries = false) {
     const unsigned k = code->k;
     if (!index) return set_status(FEC_EINVAL, "index is NULL");
-    std::vector<unsigned char> seen(256, 0);
+    unsigned char seen[256] = {};
     for (unsigned i = 0; i < k; ++i) {
         if (index[i] >= code->n)
             return set_status(FEC_EINVAL, "block number %u out of range (n = %u)", index[i], unsigned(code->n));
@@ -1263,7 +906,8 @@ int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& 
         if (index[i] < k && index[i] != i)
             return set_status(FEC_EINVAL, "primary block %u must be at slot %u, found at slot %u", index[i], index[i], i);
     }
-    std::vector<uint8_t> dec(size_t(k) * k);
+    thread_local std::vector<uint8_t> dec;
+    dec.resize(size_t(k) * k);
     if (!build_decode_matrix(code->enc_matrix, k, index, dec.data()))
         return set_status(FEC_ESINGULAR, "decode matrix is singular");
     rows.clear();
@@ -1276,11 +920,18 @@ int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& 
     return FEC_OK;
 }
 
-int encode_rows(const fec_t* code, const unsigned* nums, size_t num, std::vector<uint8_t>& rows) {
+// The encoding matrix rows of block_nums (num x k): consecutive ascending
+// numbers are one contiguous run of enc_matrix (used in place), others are
+// gathered into the thread's buffer.
+const uint8_t* encode_rows(const fec_t* code, const unsigned* nums, size_t num) {
     const unsigned k = code->k;
+    bool run = true;
+    for (size_t i = 1; i < num && run; ++i) run = nums[i] == nums[0] + i;
+    if (run) return code->enc_matrix + size_t(nums[0]) * k;
+    thread_local std::vector<uint8_t> rows;
     rows.resize(num * k);
     for (size_t i = 0; i < num; ++i) std::memcpy(&rows[i * k], code->enc_matrix + size_t(nums[i]) * k, k);
-    return FEC_OK;
+    return rows.data();
 }
 
 }  // namespace
@@ -1343,9 +994,8 @@ FEC_API int fec_encode_ex(const fec_t* code, const gf* const* src, gf* const* fe
     if (num_block_nums == 0) return set_status(FEC_OK);
     if (!src || !fecs) return set_status(FEC_EINVAL, "NULL block array");
     return guarded([&] {
-        std::vector<uint8_t> rows;
-        encode_rows(code, block_nums, num_block_nums, rows);
-        return run_single(rows.data(), code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
+        const uint8_t* rows = encode_rows(code, block_nums, num_block_nums);
+        return run_single(rows, code->k, static_cast<unsigned>(num_block_nums), src, fecs, sz, stream, flags);
     });
 }
 
@@ -1357,12 +1007,8 @@ namespace {
 // ZFEC_HIP_QUIET=1 silences it); fec_last_status() still holds every one.
 void report_void_failure(const char* fn, int st) {
     static std::atomic<int> reported[2] = {{0}, {0}};
-    static const bool quiet = [] {
-        const char* v = getenv("ZFEC_HIP_QUIET");
-        return v && v[0] == '1';
-    }();
     std::atomic<int>& once = reported[fn[4] == 'd' ? 1 : 0];
-    if (quiet || once.exchange(1) != 0) return;
+    if (config().quiet || once.exchange(1) != 0) return;
     fprintf(stderr,
             "zfec_hip: %s failed (status %d: %s); its output blocks are not valid.  Further failures of %s are "
             "not reported here; fec_last_status() / fec_last_error_message() give each call's status.\n",
@@ -1380,7 +1026,7 @@ FEC_API void fec_encode(const fec_t* code, const gf* const* src, gf* const* fecs
 FEC_API int fec_decode_ex(const fec_t* code, const gf* const* inpkts, gf* const* outpkts, const unsigned* index,
                           size_t sz, void* stream, unsigned flags) {
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
-    std::vector<uint8_t> rows;
+    thread_local std::vector<uint8_t> rows;
     unsigned r = 0;
     if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0) return set_status(FEC_OK);
@@ -1472,15 +1118,27 @@ FEC_API int fec_jit_wait(void) {
     return jit_wait();
 }
 
+FEC_API int fec_reload_config(void) {
+    reload_config();
+    return set_status(FEC_OK);
+}
+
+FEC_API int fec_last_wait(void) { return t_last_wait; }
+
 namespace {
-// Compile the specialised kernels apply_matrix would launch for this r x k
-// matrix: its row groups of one launch each (codes with k <= kMaxIn; wider
-// codes run XOR-accumulating passes, which the table kernels serve).
+// Compile the specialised kernels apply_matrix_range would launch for this
+// r x k matrix in large launches: its row groups of one launch each (the same
+// near-equal groups).  Groups past kJitMaxCoef coefficients run on
+// matapply_bsg and need no compile.
 int prepare_rows(const uint8_t* coef, unsigned k, unsigned r) {
-    if (k > static_cast<unsigned>(kMaxIn) || r == 0) return set_status(FEC_OK);
-    const unsigned rmax = std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / k));
-    for (unsigned i0 = 0; i0 < r; i0 += rmax) {
-        const unsigned rg = std::min<unsigned>(rmax, r - i0);
+    if (r == 0) return set_status(FEC_OK);
+    const bool wide = k > static_cast<unsigned>(kMaxIn);
+    const unsigned rmax =
+        wide ? static_cast<unsigned>(kMaxOut) : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / k));
+    const unsigned ngroups = (r + rmax - 1) / rmax;
+    for (unsigned g = 0; g < ngroups; ++g) {
+        const unsigned i0 = g * r / ngroups, rg = (g + 1) * r / ngroups - i0;
+        if (k * rg > kJitMaxCoef) continue;
         if (jit_prepare(coef + size_t(i0) * k, k, rg) != 0)
             return set_status(FEC_EHIP, "JIT compile failed: %s", jit_last_error().c_str());
     }
@@ -1491,9 +1149,8 @@ int prepare_rows(const uint8_t* coef, unsigned k, unsigned r) {
 FEC_API int fec_jit_prepare_encode(const fec_t* code, const unsigned* block_nums, size_t num_block_nums) {
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
     if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
-    std::vector<uint8_t> rows;
-    encode_rows(code, block_nums, num_block_nums, rows);
-    return prepare_rows(rows.data(), code->k, static_cast<unsigned>(num_block_nums));
+    if (num_block_nums == 0) return set_status(FEC_OK);
+    return prepare_rows(encode_rows(code, block_nums, num_block_nums), code->k, static_cast<unsigned>(num_block_nums));
 }
 
 FEC_API int fec_jit_prepare_decode(const fec_t* code, const unsigned* index, unsigned flags) {
@@ -1510,12 +1167,13 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     const unsigned k = code->k;
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
     if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    // one pointer query per side: device memory (its device), or host memory
+    const int sdev = pointer_device(src), ddev0 = pointer_device(dst);
     // pageable host memory on either side: staged through pinned slots
     // (synchronous whatever the flags; FEC_FLAG_ROW_PADDING does not apply)
-    if (sz && nstripes && r) {
+    if (sz && nstripes && r && (sdev < 0 || ddev0 < 0)) {
         const size_t src_ext = (nstripes - 1) * sss + (k - 1) * sbs + sz;
         const size_t dst_ext = (nstripes - 1) * dss + (r - 1) * dbs + sz;
-        const int sdev = pointer_device(src), ddev0 = pointer_device(dst);
         const uint8_t* zs = sdev >= 0 ? src : mapped_block(src, src_ext);
         const uint8_t* zd = ddev0 >= 0 ? dst : mapped_block(dst, dst_ext);
         if (!zs || !zd) {
@@ -1536,10 +1194,7 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so
     // one long-stream launch replaces the walk over short rows.
     // (ZFEC_HIP_BATCH_COLLAPSE=0 turns this off, for A/B runs.)
-    static const bool collapse = [] {
-        const char* v = getenv("ZFEC_HIP_BATCH_COLLAPSE");
-        return !(v && v[0] == '0');
-    }();
+    const bool collapse = config().batch_collapse;
     // FEC_FLAG_ROW_PADDING: run the rows out to a whole 128-byte line where the
     // strides leave room.  A row ending mid-line leaves a partly written line
     // that HBM completes with a read-modify-write: 10^6 K=3/M=10 stripes of
@@ -1565,8 +1220,8 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     // device memory on one device, or page-locked host memory (zero-copy)
     const size_t src_extent = (nstripes - 1) * sss + (k - 1) * sbs + sz;
     const size_t dst_extent = (nstripes - 1) * dss + (r - 1) * dbs + sz;
-    int dev = pointer_device(src);
-    const int ddev = pointer_device(dst);
+    int dev = sdev;
+    const int ddev = ddev0;
     if (dev < 0) {
         const uint8_t* z = mapped_block(src, src_extent);
         if (!z) return set_status(FEC_EINVAL, "batched entry points take device or page-locked host memory");
@@ -1585,11 +1240,11 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     DevCtx* d = nullptr;
     if (dev_ctx(dev, &d)) return t_status;
     hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
-    std::vector<const uint8_t*> in(k);
-    std::vector<uint8_t*> out(r);
+    const uint8_t* in[kMaxWideIn];
+    uint8_t* out[kMaxWideIn];
     for (unsigned j = 0; j < k; ++j) in[j] = src + j * sbs;
     for (unsigned i = 0; i < r; ++i) out[i] = dst + i * dbs;
-    if (apply_matrix(coef, k, r, in.data(), out.data(), sz, nstripes, sss, dss, st)) return t_status;
+    if (apply_matrix(coef, k, r, in, out, sz, nstripes, sss, dss, st)) return t_status;
     if (!(flags & FEC_FLAG_ASYNC)) {
         hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -1605,10 +1260,9 @@ FEC_API int fec_encode_batch(const fec_t* code, const gf* src, size_t src_block_
     if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
     if (num_block_nums == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
     return guarded([&] {
-        std::vector<uint8_t> rows;
-        encode_rows(code, block_nums, num_block_nums, rows);
-        return run_batch(code, rows.data(), static_cast<unsigned>(num_block_nums), src, src_block_stride,
-                         src_stripe_stride, dst, dst_block_stride, dst_stripe_stride, sz, nstripes, stream, flags);
+        return run_batch(code, encode_rows(code, block_nums, num_block_nums), static_cast<unsigned>(num_block_nums),
+                         src, src_block_stride, src_stripe_stride, dst, dst_block_stride, dst_stripe_stride, sz,
+                         nstripes, stream, flags);
     });
 }
 
@@ -1616,12 +1270,159 @@ FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_
                              gf* dst, size_t dst_block_stride, size_t dst_stripe_stride, const unsigned* index,
                              size_t sz, size_t nstripes, void* stream, unsigned flags) {
     if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
-    std::vector<uint8_t> rows;
+    thread_local std::vector<uint8_t> rows;
     unsigned r = 0;
     if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
     if (r == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
     return guarded([&] {
         return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
                          dst_stripe_stride, sz, nstripes, stream, flags);
+    });
+}
+
+// ============================================================================
+// Several GPUs of one process: a batch's stripes are
+// independent (zfec/fec.c:494-503 touches one column range of each block), so
+// the batch is split into contiguous balanced stripe ranges, one per listed
+// device, each run by a persistent host thread bound to that device with its
+// own stream and staging slots -- the reference's only parallelism is the
+// same thing on CPU threads (the GIL released around fec_encode,
+// zfec/_fecmodule.c:221-223).  Host memory only: each GPU reads and writes
+// its share over its own PCIe link; device-resident batches stay on their
+// device (one fec_encode_batch per device).
+// ============================================================================
+namespace {
+
+// One persistent thread per (device, position in the call's device list): the
+// thread-local contexts (streams, pinned slots) it builds on first use are
+// kept for later calls.
+class DevWorker {
+public:
+    explicit DevWorker(int dev) : dev_(dev), th_([this] { loop(); }) {}
+    void post(std::function<void()> fn) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(fn));
+        }
+        cv_.notify_one();
+    }
+
+private:
+    void loop() {
+        (void)hipSetDevice(dev_);
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [this] { return !q_.empty(); });
+            std::function<void()> fn = std::move(q_.front());
+            q_.pop_front();
+            lk.unlock();
+            fn();
+            lk.lock();
+        }
+    }
+    int dev_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::thread th_;
+};
+
+DevWorker& dev_worker(int dev, size_t pos) {
+    // lives for the process (workers may be parked at exit); a forked child
+    // builds its own
+    static std::mutex m;
+    static std::map<std::pair<int, size_t>, DevWorker*>* workers = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> g(m);
+    if (!workers || owner != getpid()) {
+        workers = new std::map<std::pair<int, size_t>, DevWorker*>;
+        owner = getpid();
+    }
+    DevWorker*& w = (*workers)[{dev, pos}];
+    if (!w) w = new DevWorker(dev);
+    return *w;
+}
+
+struct ShardResult {
+    int status = FEC_OK;
+    char msg[256] = "";
+};
+
+int run_batch_multi(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src, size_t sbs, size_t sss,
+                    gf* dst, size_t dbs, size_t dss, size_t sz, size_t nstripes, const int* devices, size_t ndev,
+                    unsigned flags) {
+    const int ngpu = gpu_available();
+    if (!ngpu) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
+    if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    if (!devices || ndev == 0) return set_status(FEC_EINVAL, "no devices listed");
+    for (size_t d = 0; d < ndev; ++d)
+        if (devices[d] < 0 || devices[d] >= ngpu)
+            return set_status(FEC_EINVAL, "device %d out of range (%d visible)", devices[d], ngpu);
+    if (pointer_device(src) >= 0 || pointer_device(dst) >= 0)
+        return set_status(FEC_EINVAL,
+                          "multi-device calls take host memory (device-resident batches: one call per device)");
+    std::vector<ShardResult> res(ndev);
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t left = 0;
+    // stripes [s0, s1) of shard d: balanced contiguous ranges (zfec_amd/shard.py shard_range)
+    const size_t base = nstripes / ndev, extra = nstripes % ndev;
+    for (size_t d = 0; d < ndev; ++d) {
+        const size_t s0 = d * base + std::min(d, extra), n = base + (d < extra ? 1 : 0);
+        if (n == 0) continue;
+        ++left;
+        const gf* ps = src + s0 * sss;
+        gf* pd = dst + s0 * dss;
+        ShardResult* out = &res[d];
+        const int dev = devices[d];
+        dev_worker(dev, d).post([=, &mu, &cv, &left] {
+            (void)hipSetDevice(dev);
+            const int st = guarded([&] {
+                return run_batch(code, coef, r, ps, sbs, sss, pd, dbs, dss, sz, n, nullptr,
+                                 (flags & ~FEC_FLAG_ASYNC) | FEC_FLAG_LIBRARY_STREAM);
+            });
+            out->status = st;
+            if (st != FEC_OK) snprintf(out->msg, sizeof out->msg, "device %d: %s", dev, t_msg);
+            std::lock_guard<std::mutex> g(mu);
+            if (--left == 0) cv.notify_all();
+        });
+    }
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left == 0; });
+    }
+    for (const ShardResult& r0 : res)
+        if (r0.status != FEC_OK) return set_status(r0.status, "%s", r0.msg);
+    return set_status(FEC_OK);
+}
+
+}  // namespace
+
+FEC_API int fec_encode_batch_multi(const fec_t* code, const gf* src, size_t src_block_stride,
+                                   size_t src_stripe_stride, gf* dst, size_t dst_block_stride,
+                                   size_t dst_stripe_stride, const unsigned* block_nums, size_t num_block_nums,
+                                   size_t sz, size_t nstripes, const int* devices, size_t ndevices, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    if (check_block_nums(code, block_nums, num_block_nums)) return t_status;
+    if (num_block_nums == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
+    return guarded([&] {
+        return run_batch_multi(code, encode_rows(code, block_nums, num_block_nums),
+                               static_cast<unsigned>(num_block_nums), src, src_block_stride, src_stripe_stride, dst,
+                               dst_block_stride, dst_stripe_stride, sz, nstripes, devices, ndevices, flags);
+    });
+}
+
+FEC_API int fec_decode_batch_multi(const fec_t* code, const gf* src, size_t src_block_stride,
+                                   size_t src_stripe_stride, gf* dst, size_t dst_block_stride,
+                                   size_t dst_stripe_stride, const unsigned* index, size_t sz, size_t nstripes,
+                                   const int* devices, size_t ndevices, unsigned flags) {
+    if (!valid_code(code)) return set_status(FEC_EINVAL, "invalid fec_t");
+    thread_local std::vector<uint8_t> rows;
+    unsigned r = 0;
+    if (decode_rows(code, index, rows, r, (flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
+    if (r == 0 || sz == 0 || nstripes == 0) return set_status(FEC_OK);
+    return guarded([&] {
+        return run_batch_multi(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
+                               dst_stripe_stride, sz, nstripes, devices, ndevices, flags);
     });
 }

@@ -1,6 +1,7 @@
 // gf256.cpp -- host GF(2^8) arithmetic and code matrices (see gf256.hpp).
 #include "gf256.hpp"
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <utility>
@@ -11,7 +12,7 @@ namespace zfec_hip {
 namespace {
 Field g_field;
 std::once_flag g_once;
-bool g_ready = false;
+std::atomic<bool> g_ready{false};  // read by fec_new on any thread
 
 // Reduction polynomial x^8+x^4+x^3+x^2+1; zfec/fec.c:16 writes it as the
 // coefficient string "101110001".
@@ -33,12 +34,12 @@ void build_field() {
     for (int a = 0; a < 256; ++a)
         for (int b = 0; b < 256; ++b)
             f.mul[a][b] = (a == 0 || b == 0) ? 0 : f.exp[f.log[a] + f.log[b]];
-    g_ready = true;
+    g_ready.store(true, std::memory_order_release);
 }
 }  // namespace
 
 void field_init() { std::call_once(g_once, build_field); }
-bool field_ready() { return g_ready; }
+bool field_ready() { return g_ready.load(std::memory_order_acquire); }
 const Field& field() {
     field_init();
     return g_field;
@@ -102,7 +103,8 @@ bool invert_matrix(uint8_t* a, unsigned k) {
     // pivot order yields the reference's bytes.
     const Field& f = field();
     const size_t w = 2 * static_cast<size_t>(k);
-    std::vector<uint8_t> aug(static_cast<size_t>(k) * w, 0);
+    thread_local std::vector<uint8_t> aug;  // reused: no allocation per decode call
+    aug.assign(static_cast<size_t>(k) * w, 0);
     for (unsigned r = 0; r < k; ++r) {
         std::memcpy(&aug[r * w], a + static_cast<size_t>(r) * k, k);
         aug[r * w + k + r] = 1;

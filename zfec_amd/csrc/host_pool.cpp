@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 
 namespace zfec_hip {
 
@@ -54,8 +55,15 @@ HostPool& HostPool::get() {
 }
 
 HostPool::HostPool(unsigned nthreads) {
-    // the caller of wait() is one of the copying threads
-    for (unsigned i = 1; i < nthreads; ++i) workers_.emplace_back([this] { worker(); });
+    // the caller of wait() is one of the copying threads; if the system cannot
+    // create them all, the pool keeps the ones it got (at least the caller)
+    for (unsigned i = 1; i < nthreads; ++i) {
+        try {
+            workers_.emplace_back([this] { worker(); });
+        } catch (const std::exception&) {
+            break;
+        }
+    }
 }
 
 HostPool::~HostPool() {

@@ -14,15 +14,20 @@
 //   * partial products are merged by v_bitop3_b32 (gfx950's 3-input logic
 //     op; truth table 0x96 = XOR3).
 //
-// Two shapes of kernel:
+// Kernel families:
 //   matapply_reg<K, R>  compile-time k <= 4 and r <= 8 (encode K=3/M=10 is
-//                       <3,7>, its decode <3,3>): all K*R tables arrive in the
-//                       kernel arguments and stay in registers; the per-chunk
-//                       body is straight-line code.
+//                       <3,7>, its decode <3,3>): all K*R tables arrive in a
+//                       kernel argument block sized to them (RegJob) and stay
+//                       in registers; the per-chunk body is straight-line code.
+//   matapply_rows<K, R> the same arithmetic, one wave per stripe of short blocks.
 //   matapply_lds        any k <= 32, r <= 48 (longer codes are split by the
 //                       caller): each workgroup expands its coefficients into
 //                       LDS tables from a compile-time bank of all 256 values;
 //                       rows in register tiles, inputs in prefetched groups.
+//   matapply_bsg        bit-sliced, coefficients as run-time data, k <= 256
+//                       (past 32 inputs its pointers and coefficients come
+//                       from a device-side table).
+//   matapply_small      launches too small to fill the chip, wide codes.
 //
 // Measured issue rates on gfx950 (tools/mb_valu.hip): v_perm_b32 and
 // v_bitop3_b32 (VOP3) sustain ~37 T lane-ops/s chip-wide, plain VOP2 ops
@@ -35,12 +40,16 @@
 #include <hip/hip_runtime.h>
 
 #include "bitslice.hpp"
+#include "config.hpp"
 
+#include <array>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
+#include <utility>
 
 namespace zfec_hip {
 namespace {
@@ -97,19 +106,13 @@ constexpr TableBank make_bank() {
 
 __constant__ TableBank g_bank = make_bank();
 
-// Host copy of the bank: launch_matapply places small launches' tables
-// directly in the kernel arguments.
+// Host copy of the bank: the register kernels get their coefficients'
+// tables in the kernel arguments.
 constexpr TableBank kHostBank = make_bank();
 
 struct Tab {
     uint32_t w0, w1, w2, w3, w4;
 };
-
-// Table of coefficient i (row-major r x k) from the kernel arguments.
-__device__ __forceinline__ Tab karg_table(const MatJob& job, uint32_t i) {
-    const uint32_t* t = &job.tab[i * 5];
-    return Tab{t[0], t[1], t[2], t[3], t[4]};
-}
 
 // ---- arithmetic ---------------------------------------------------------------
 
@@ -159,20 +162,17 @@ __device__ __forceinline__ void store16_out(uint8_t* p, u32x4 v) {
         store16(p, v);
 }
 
-// Output store with an explicit cache policy (SP != 0; tools/mb_store.hip):
-// 1 = sc1, 2 = sc0 sc1, 3 = nt sc1.  SP = 0 defers to store16_out<NT>.  The
-// trailing s_nop keeps the compiler's next instruction from overwriting the
-// data registers before the store has read them.
-template <bool NT, int SP>
+// Output store of the register kernels: SP = 0 streams it (nt), SP = 3
+// streams it and writes it through the L2 at device scope (nt sc1; the
+// single-stripe store policy, kernels dispatch below).  The trailing s_nop
+// keeps the compiler's next instruction from overwriting the data registers
+// before the store has read them.
+template <int SP>
 __device__ __forceinline__ void store16_pol(uint8_t* p, u32x4 v) {
-    if constexpr (SP == 1)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (SP == 2)
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else if constexpr (SP == 3)
+    if constexpr (SP == 3)
         asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else
-        store16_out<NT>(p, v);
+        store16_out<true>(p, v);
 }
 
 // The last (sz % 16) bytes of a block.
@@ -188,26 +188,18 @@ __device__ inline void store_tail(uint8_t* p, u32x4 v, uint32_t nb) {
 }
 
 // Walks this lane's (stripe, chunk) units in grid-stride order without a
-// division per step.
-// XCD-contiguous workgroup order: workgroups are dealt round-robin over the
-// 8 XCDs (blockIdx % 8 share one); renumbering them so that each XCD's share
-// is one contiguous range of the walk lets each XCD stream its own eighth of
-// every block (a bijection on [0, gridDim.x); MI355X_MICROARCH.md, workgroup
-// dispatch).
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nwg) {
-    const uint32_t q = nwg / 8, rr = nwg % 8, x = b % 8;
-    return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + b / 8;
-}
-
+// division per step.  (An XCD-contiguous workgroup order measured 2 % slower
+// on 256 x 1 MiB K=3/M=10 encodes from cold caches, profiles/r02_mb_cold.log.)
 struct UnitIter {
     uint32_t s, c;
-    __device__ explicit UnitIter(const MatJob& job) {
-        const uint32_t wg = job.xcd_swizzle ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-        const uint32_t gid = wg * kBlock + threadIdx.x;
+    template <class J>
+    __device__ explicit UnitIter(const J& job) {
+        const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
         s = gid / job.cps;
         c = gid - s * job.cps;
     }
-    __device__ __forceinline__ void next(const MatJob& job) {
+    template <class J>
+    __device__ __forceinline__ void next(const J& job) {
         c += job.gs_c;
         s += job.gs_s;
         if (c >= job.cps) {
@@ -237,27 +229,47 @@ __device__ __forceinline__ Span chunk_span(uint32_t c, uint64_t sz, uint32_t nfu
     return Span{off, false, static_cast<uint32_t>(sz - off)};
 }
 
-// ---------------------------------------------------------------------------
-// matapply_reg<K, R>: compile-time k and r.  All K*R tables come with the
-// kernel arguments (prefetched scalar loads); the compiler keeps the high
-// words in SGPRs and copies the low words to VGPRs once, outside the loop.
-// ---------------------------------------------------------------------------
-// The kernel's MatJob argument read in place from the kernel-argument segment
+// A kernel's argument block read in place from the kernel-argument segment
 // through a pointer the compiler must treat as new at every call (empty asm):
 // the loads stay where they are used instead of all being hoisted into the
-// prologue, where the 5*K*R table dwords and the block pointers overflow the
-// SGPRs and spill to VGPR lanes (v_writelane / v_readlane per wave).
-typedef const __attribute__((address_space(4))) MatJob* KJob;
-__device__ __forceinline__ KJob kernarg_job() {
-    KJob kj = (KJob)__builtin_amdgcn_kernarg_segment_ptr();
+// prologue, where the table dwords and the block pointers overflow the SGPRs
+// and spill to VGPR lanes (v_writelane / v_readlane per wave).
+template <class J>
+using KPtr = const __attribute__((address_space(4))) J*;
+
+template <class J>
+__device__ __forceinline__ KPtr<J> kernarg_job() {
+    KPtr<J> kj = (KPtr<J>)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kj));
     return kj;
 }
 
+// ---------------------------------------------------------------------------
+// matapply_reg<K, R>: compile-time k and r.  The kernel argument block holds
+// the K + R block pointers and the K*R coefficients' tables (5 dwords each):
+// 560 bytes for <3,7>, against 2.2 KiB for the table kernels' MatJob.
+// ---------------------------------------------------------------------------
+template <int K, int R>
+struct alignas(16) RegJob {
+    uint64_t sz, in_sstride, out_sstride;
+    uint32_t nstripes, cps, gs_c, gs_s;
+    uint32_t* done_flag;  // pinned host word a one-workgroup launch stores done_seq into when finished
+    uint32_t done_seq, pad_;
+    const uint8_t* in[K];
+    uint8_t* out[R];
+    uint32_t tab[K * R * 5];
+};
+
+template <int K, int R>
+__device__ __forceinline__ Tab reg_table(const RegJob<K, R>& job, uint32_t i) {
+    const uint32_t* t = &job.tab[i * 5];
+    return Tab{t[0], t[1], t[2], t[3], t[4]};
+}
+
 // One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.  AL: each
 // row's tables and output pointer are loaded (scalar loads) right before use.
-template <int K, int R, bool NT, int SP = 0, bool AL = false>
-__device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
+template <int K, int R, int SP, bool AL>
+__device__ __forceinline__ void reg_compute_store(const RegJob<K, R>& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
                                                   uint64_t ob, bool full, uint32_t nb) {
     Sel sel[4][K];
 #pragma unroll
@@ -272,7 +284,7 @@ __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (
         Tab t[K];
         uint8_t* out;
         if constexpr (AL) {
-            const KJob kj = kernarg_job();
+            const KPtr<RegJob<K, R>> kj = kernarg_job<RegJob<K, R>>();
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t i = (r * K + j) * 5;
@@ -286,14 +298,15 @@ __device__ __forceinline__ void reg_compute_store(const MatJob& job, const Tab (
         }
         const u32x4 y{gf_dot<K>(t, sel[0]), gf_dot<K>(t, sel[1]), gf_dot<K>(t, sel[2]), gf_dot<K>(t, sel[3])};
         if (full)
-            store16_pol<NT, SP>(out + ob, y);
+            store16_pol<SP>(out + ob, y);
         else
             store_tail(out + ob, y, nb);
     }
 }
 
-template <int K>
-__device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint64_t ib, bool full, uint32_t nb) {
+template <int K, int R>
+__device__ __forceinline__ void reg_load(const RegJob<K, R>& job, u32x4 (&x)[K], uint64_t ib, bool full,
+                                         uint32_t nb) {
     if (full) {
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + ib);
@@ -303,38 +316,37 @@ __device__ __forceinline__ void reg_load(const MatJob& job, u32x4 (&x)[K], uint6
     }
 }
 
-// U: units per lane per loop trip (U = 2 puts 2K loads in flight per lane).
-// PF (U = 1 only): the next unit's inputs are loaded before the current unit
-// is computed, so a lane with several units (grid-stride) keeps loads in
-// flight while it computes (tools/mb_encode.hip, variants "PF").
-// W: __launch_bounds__ waves-per-SIMD floor (0: none; tools/mb_encode.hip variants "W8").
-// AL: tables and output pointers read where they are used (reg_compute_store).
-template <int K, int R, bool NT, int U = 1, int SP = 0, bool PF = false, int W = 0, bool AL = false>
-__global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJob job) {
+// PF: the next unit's inputs are loaded before the current unit is computed,
+// so a lane with several units (grid-stride) keeps loads in flight while it
+// computes (tools/mb_encode.hip, variants "PF"; 5-8 rows only: from cold
+// caches the 3-row decode is slower with it, profiles/r02_reg_pf_ab.log).
+// SP: output store policy (store16_pol).  AL: tables and output pointers read
+// where they are used (reg_compute_store).
+template <int K, int R, int SP, bool PF, bool AL>
+__global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
     Tab T[R][K];
     if constexpr (!AL) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int j = 0; j < K; ++j) T[r][j] = karg_table(job, r * K + j);
+            for (int j = 0; j < K; ++j) T[r][j] = reg_table(job, r * K + j);
     }
 
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
     UnitIter u(job);
     if constexpr (PF) {
-        static_assert(U == 1, "prefetch walks one unit per trip");
         u32x4 x[K];
         Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
         uint64_t ob = u.s * job.out_sstride + sp.off;
-        if (u.s < job.nstripes) reg_load<K>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
+        if (u.s < job.nstripes) reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
         while (u.s < job.nstripes) {
             UnitIter v = u;
             v.next(job);
             const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
             u32x4 xn[K];
-            if (v.s < job.nstripes) reg_load<K>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
-            reg_compute_store<K, R, NT, SP, AL>(job, T, x, ob, sp.full, sp.nb);
+            if (v.s < job.nstripes) reg_load<K, R>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
+            reg_compute_store<K, R, SP, AL>(job, T, x, ob, sp.full, sp.nb);
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = xn[j];
             sp = spn;
@@ -342,26 +354,13 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
             u = v;
         }
     } else {
-    while (u.s < job.nstripes) {
-        uint64_t ib[U], ob[U];
-        uint32_t nb[U];
-        bool full[U], live[U];
-        u32x4 x[U][K];
-#pragma unroll
-        for (int i = 0; i < U; ++i) {
-            live[i] = u.s < job.nstripes;
+        while (u.s < job.nstripes) {
             const Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
-            ib[i] = u.s * job.in_sstride + sp.off;
-            ob[i] = u.s * job.out_sstride + sp.off;
-            full[i] = sp.full;
-            nb[i] = sp.nb;
-            if (live[i]) reg_load<K>(job, x[i], ib[i], full[i], nb[i]);
+            u32x4 x[K];
+            reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
+            reg_compute_store<K, R, SP, AL>(job, T, x, u.s * job.out_sstride + sp.off, sp.full, sp.nb);
             u.next(job);
         }
-#pragma unroll
-        for (int i = 0; i < U; ++i)
-            if (live[i]) reg_compute_store<K, R, NT, SP, AL>(job, T, x[i], ob[i], full[i], nb[i]);
-    }
     }
     // one-workgroup launches of a synchronous small call: publish completion
     // in pinned host memory (every wave's stores complete at system scope,
@@ -382,48 +381,39 @@ __global__ __launch_bounds__(kBlock, W > 0 ? W : 1) void matapply_reg(const MatJ
 // one contiguous piece of one block.  The stripe-major unit walk of
 // matapply_reg would let a wave instruction straddle the end of one stripe's
 // block and the start of the next one's (two DRAM rows); at K=3/M=10 with
-// 1366-byte blocks the row walk is 5 % faster (tools/mb_rows.hip).
+// 1366-byte blocks the row walk is 5 % faster (tools/mb_rows.hip).  Every
+// piece of the lane's share of the stripe (at most 4) is loaded before any is
+// computed, so all of the wave's loads are in flight at once (cfg5 encode
+// 67.7 -> 70.1 % of HBM cold, decode 66.7 -> 69.8 %, profiles/r02_rows_pre_ab.log).
 // ---------------------------------------------------------------------------
 constexpr uint64_t kRowsMin = 1024, kRowsMax = 4096;
 
-template <int K, int R, bool AL, bool PRE = false>
-__global__ __launch_bounds__(kBlock) void matapply_rows(const MatJob job) {
+template <int K, int R, bool AL>
+__global__ __launch_bounds__(kBlock) void matapply_rows(const RegJob<K, R> job) {
     Tab T[R][K];
     if constexpr (!AL) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int j = 0; j < K; ++j) T[r][j] = karg_table(job, r * K + j);
+            for (int j = 0; j < K; ++j) T[r][j] = reg_table(job, r * K + j);
     }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t waves = gridDim.x * (kBlock / 64);
     const uint64_t sz = job.sz;
     for (uint32_t s = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); s < job.nstripes; s += waves) {
-        if constexpr (PRE) {
-            // PRE (default): every piece of the lane's share of the stripe (at
-            // most 4: sz <= 4 KiB) loaded before any is computed, so all of the
-            // wave's loads are in flight at once
-            u32x4 x[4][K];
-            uint64_t o[4];
-            bool live[4];
+        u32x4 x[4][K];
+        uint64_t o[4];
+        bool live[4];
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const uint64_t off = lane * 16u + 1024u * h;
-                live[h] = off < sz;
-                o[h] = off + 16u <= sz ? off : sz - 16u;
-                if (live[h]) reg_load<K>(job, x[h], s * job.in_sstride + o[h], true, 16u);
-            }
-#pragma unroll
-            for (int h = 0; h < 4; ++h)
-                if (live[h]) reg_compute_store<K, R, true, 0, AL>(job, T, x[h], s * job.out_sstride + o[h], true, 16u);
-        } else {
-            for (uint64_t off = lane * 16u; off < sz; off += 1024u) {
-                const uint64_t o = off + 16u <= sz ? off : sz - 16u;
-                u32x4 x[K];
-                reg_load<K>(job, x, s * job.in_sstride + o, true, 16u);
-                reg_compute_store<K, R, true, 0, AL>(job, T, x, s * job.out_sstride + o, true, 16u);
-            }
+        for (int h = 0; h < 4; ++h) {
+            const uint64_t off = lane * 16u + 1024u * h;
+            live[h] = off < sz;
+            o[h] = off + 16u <= sz ? off : sz - 16u;
+            if (live[h]) reg_load<K, R>(job, x[h], s * job.in_sstride + o[h], true, 16u);
         }
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+            if (live[h]) reg_compute_store<K, R, 0, AL>(job, T, x[h], s * job.out_sstride + o[h], true, 16u);
     }
 }
 
@@ -579,9 +569,7 @@ __host__ __device__ constexpr uint32_t table_rows(uint32_t r, uint32_t rt) {
     return MODE == kTilesPadded ? (r + rt - 1) / rt * rt : r;
 }
 
-// PROBE (microbenchmarks only, tools/mb_encode.hip): 1 = no memory traffic
-// (inputs synthesised, outputs dropped), 2 = no arithmetic (XOR of inputs).
-template <bool ACC, bool NT, int RT_, int D, int GG, int MODE, int PROBE = 0>
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE>
 __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     constexpr uint32_t CH = 4 * D;
     extern __shared__ LdsTab lds_tab[];
@@ -601,14 +589,7 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
         const uint64_t ib = st.u.s * job.in_sstride + sp.off;
 #pragma unroll
         for (int jj = 0; jj < GG; ++jj)
-            if (st.g + jj < k) {
-                if constexpr (PROBE == 1) {
-#pragma unroll
-                    for (int v = 0; v < D; ++v) x[jj].w[v] = static_cast<uint32_t>(ib) * 0x9E3779B9u + st.g + jj + v;
-                } else {
-                    x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
-                }
-            }
+            if (st.g + jj < k) x[jj] = load_words<D>(job.in[st.g + jj] + ib, sp.full, sp.nb);
     };
     Step cur{UnitIter(job), 0u, 0u};
     bool live = cur.u.s < job.nstripes;
@@ -643,14 +624,7 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
         Words<D> xb[GG];
         if (nlive) load_step(nxt, xb);
         if (live) {
-            if constexpr (PROBE == 2) {
-#pragma unroll
-                for (int jj = 0; jj < GG; ++jj)
-#pragma unroll
-                    for (int v = 0; v < D; ++v) a[jj % RT_][v] ^= xa[jj].w[v];
-            } else {
-                mac_group<MODE == kTilesPadded, RT_, D, GG>(a, xa, lds_tab, cur.g, cur.rb, k, rp);
-            }
+            mac_group<MODE == kTilesPadded, RT_, D, GG>(a, xa, lds_tab, cur.g, cur.rb, k, rp);
             if (tile_end) {
                 const Span sp = chunk_span<CH, !ACC>(cur.u.c, sz, nfull);
                 const uint64_t ob = cur.u.s * job.out_sstride + sp.off;
@@ -666,11 +640,7 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
 #pragma unroll
                         for (int v = 0; v < D; ++v) y.w[v] ^= o.w[v];
                     }
-                    if constexpr (PROBE == 1) {
-                        if (y.w[0] == 0x12345678u && y.w[D - 1] == 0x9abcdef0u) store_words<D, NT>(op, y, sp.full, sp.nb);
-                    } else {
-                        store_words<D, NT>(op, y, sp.full, sp.nb);
-                    }
+                    store_words<D, NT>(op, y, sp.full, sp.nb);
                 }
             }
         }
@@ -687,14 +657,15 @@ __device__ __forceinline__ void matapply_lds_body(const MatJob& job) {
     }
 }
 
-template <bool ACC, bool NT, int RT_, int D, int GG, int MODE = kTilesRagged, int PROBE = 0>
+template <bool ACC, bool NT, int RT_, int D, int GG, int MODE = kTilesRagged>
 __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
-    matapply_lds_body<ACC, NT, RT_, D, GG, MODE, PROBE>(job);
+    matapply_lds_body<ACC, NT, RT_, D, GG, MODE>(job);
 }
 
 // ---------------------------------------------------------------------------
-// matapply_bsg<RT, P>: bit-sliced, with the coefficient matrix as run-time data
-// (no compile step: every erasure pattern runs at this speed the first time).
+// matapply_bsg<RT, TBL>: bit-sliced, with the coefficient matrix as run-time
+// data (no compile step: every erasure pattern runs at this speed the first
+// time).
 //
 // Multiplication by c is an 8x8 GF(2) matrix on the bits of a byte.  After an
 // 8x8 bit transpose a lane's 32 bytes are 8 bit-planes p0..p7, and output
@@ -710,14 +681,23 @@ __global__ __launch_bounds__(kBlock) void matapply_lds(const MatJob job) {
 // One workgroup (4 waves) per unit of 4 KiB of every block of a stripe: lane l
 // owns bytes 16l + 1024h (h = 0..3) of each block, two 32-byte groups (h = 0,1
 // and h = 2,3).  The r output rows are split over the 4 waves (RT rows each,
-// accumulators in registers).  Inputs go in phases of P: wave w loads input
-// j = P*phase + w, transposes it, and writes its combinations to LDS slot w;
-// after a barrier every wave folds the phase's P inputs into its rows.
-// LDS per slot: 32 combinations x 64 lanes x 8 B = 16 KiB (entries 0 and 16
-// hold zeros, written once).
+// accumulators in registers).  Inputs go in phases of 2: waves 0 and 1 each
+// load one input of the phase, transpose it and write its combinations to
+// their LDS slot; after a barrier every wave folds the phase's 2 inputs into
+// its rows.  LDS per slot: 32 combinations x 64 lanes x 8 B = 16 KiB (entries
+// 0 and 16 hold zeros, written once).  (Measured and not kept, DESIGN.md §4:
+// 4 inputs per phase, a scheduling barrier per row, the input build balanced
+// over all 4 waves.)
+//
+// TBL = false: block pointers and coefficients in the MatJob kernel arguments
+// (k <= 32).  TBL = true: in a device-side table the host fills per launch
+// (BsgTblJob::table: k input pointers, r output pointers, then the
+// coefficients in walk order), read with scalar loads -- k up to 256 in one
+// pass, instead of XOR-accumulating passes of 32 inputs.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBsgChunk = 4096;        // bytes of each block per unit
 constexpr uint32_t kBsgSlotBytes = 32 * 512;  // one input's combinations
+constexpr int kBsgPhase = 2;                // inputs per LDS phase
 
 // g_bsg.off[c]: sixteen dwords, the LDS byte offsets of the combinations
 // output plane b of c*x needs: [b] = L[ml_b], [8 + b] = H[mh_b] (b = 0..7).
@@ -792,40 +772,49 @@ __device__ __forceinline__ void write_combos(char* slot, uint32_t lane8, const u
     }
 }
 
-// One group's 15 nonzero combinations (BB walk: a wave builds one 32-byte
-// group of an input), dword g of each 8-byte entry.
-__device__ __forceinline__ void write_combos1(char* slot, uint32_t lane8g, const uint32_t (&q)[4], uint32_t base) {
-    uint32_t c[16];
-    c[0] = 0u;
-#pragma unroll
-    for (int m = 1; m < 16; ++m) {
-        const int top = 31 - __builtin_clz(m);
-        c[m] = c[m ^ (1 << top)] ^ q[top];
-        *reinterpret_cast<uint32_t*>(slot + (base + m) * 512u + lane8g) = c[m];
-    }
-}
-
 // Rows are interleaved over the waves: wave w owns rows w + 4*rr, rr < RT.
 // launch_bsg lays the coefficients out for this walk: wave w's bytes of phase
-// f are (js, rr) in order, js < P, rr < RT, at byte (w * nphases + f) *
-// bsg_phase_bytes(P, RT) (rows past r and inputs past k get coefficient 0,
+// f are (js, rr) in order, js < 2, rr < RT, at byte (w * nphases + f) *
+// bsg_phase_bytes(RT) (rows past r and inputs past k get coefficient 0,
 // whose combinations are the zero entries).  A coefficient's eight offset
 // dwords come from g_bsg by scalar loads, issued one step (row) ahead: a wait
 // for a scalar load also drains the wave's LDS reads, so it must come where
 // the wave has none outstanding.
-template <int P, int RT>
+template <int RT>
 __host__ __device__ constexpr uint32_t bsg_phase_bytes() {
-    return (P * RT + 3) / 4 * 4;
+    return (kBsgPhase * RT + 3) / 4 * 4;
 }
 
-// BB (P = 2 only): the build is balanced over all 4 waves, wave w transposing
-// and tabulating group w & 1 of the phase's input w >> 1 (two 16-byte loads, one
-// transpose, 15 + 15 combinations written as dwords); otherwise waves 0 and 1
-// each build both groups of one input while waves 2 and 3 wait.
-template <int RT, int P, bool SB = true, bool BB = false>
-__global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
-    static_assert(!BB || P == 2, "the balanced build pairs 4 waves with 2 inputs");
-    constexpr uint32_t PB = bsg_phase_bytes<P, RT>();
+struct alignas(16) BsgTblJob {
+    uint64_t sz, in_sstride, out_sstride;
+    uint32_t nstripes, k, r, cps, gs_c, gs_s, pad0_, pad1_;
+    const uint8_t* table;  // device memory: k input pointers, r output pointers, walk-order coefficients
+};
+
+typedef const __attribute__((address_space(4))) uint64_t* CU64;
+typedef const __attribute__((address_space(4))) uint32_t* KWords;
+
+// Block pointers and coefficient words of a launch: from the kernel arguments
+// (MatJob) or from the device-side table (scalar loads either way).
+struct BsgKarg {
+    KPtr<MatJob> kj;
+    __device__ const uint8_t* in(uint32_t j) const { return kj->in[j]; }
+    __device__ uint8_t* out(uint32_t i) const { return kj->out[i]; }
+    __device__ KWords coef() const { return (KWords)kj->coef; }
+};
+
+struct BsgTbl {
+    CU64 tp;
+    uint32_t k, r;
+    __device__ const uint8_t* in(uint32_t j) const { return reinterpret_cast<const uint8_t*>(tp[j]); }
+    __device__ uint8_t* out(uint32_t i) const { return reinterpret_cast<uint8_t*>(tp[k + i]); }
+    __device__ KWords coef() const { return (KWords)(tp + k + r); }
+};
+
+template <int RT, bool TBL, class J>
+__global__ __launch_bounds__(256) void matapply_bsg(const J job) {
+    constexpr int P = kBsgPhase;
+    constexpr uint32_t PB = bsg_phase_bytes<RT>();
     constexpr int ND = PB / 4;           // coefficient dwords per wave and phase
     extern __shared__ char bsg_lds[];    // P slots of kBsgSlotBytes
     const uint32_t lane = threadIdx.x & 63u;
@@ -838,45 +827,41 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
         const uint32_t sl = i / 128, e = (i / 64) & 1u, l = i & 63u;
         *reinterpret_cast<u32x2*>(bsg_lds + sl * kBsgSlotBytes + e * 16u * 512u + l * 8u) = u32x2{0u, 0u};
     }
-    const KJob kj = kernarg_job();
-    typedef const __attribute__((address_space(4))) uint32_t* KWords;
-    const KWords cw = (KWords)kj->coef + wave * nph * ND;  // this wave's phases
+    const auto src = [&] {
+        if constexpr (TBL)
+            return BsgTbl{(CU64)job.table, k, r};
+        else
+            return BsgKarg{kernarg_job<MatJob>()};
+    }();
+    const KWords cw = src.coef() + wave * nph * ND;  // this wave's phases
     const uint64_t sz = job.sz;
-    // byte offset of unit (s, c) in a block of stripe s: the last unit of a
-    // block ends at sz (overlapping its neighbour)
-    auto unit_off = [&](uint32_t su, uint32_t cu) {
+    // byte offset of unit c in a block: the last unit of a block ends at sz
+    // (overlapping its neighbour)
+    auto unit_off = [&](uint32_t cu) {
         uint64_t o = static_cast<uint64_t>(cu) * kBsgChunk;
         return o > sz - kBsgChunk ? sz - kBsgChunk : o;
     };
-    const bool builder = BB || wave < static_cast<uint32_t>(P);
-    const uint32_t bin = BB ? wave >> 1 : wave;        // the phase's input this wave builds
-    const uint32_t bgrp = BB ? (wave & 1u) : 0u;      // BB: its 32-byte group
+    const bool builder = wave < static_cast<uint32_t>(P);
     // the input this wave transposes next, loaded one phase ahead (the next
     // unit's first phase while the current unit's last phase computes), so a
     // phase never starts waiting on HBM
     u32x4 xin[4];
     auto load_input = [&](uint32_t su, uint32_t cu, uint32_t j) {
-        const uint8_t* ip = kj->in[j] + (su * job.in_sstride + unit_off(su, cu) + lane * 16u);
-        if constexpr (BB) {
-            xin[0] = load16(ip + 2048u * bgrp);
-            xin[1] = load16(ip + 2048u * bgrp + 1024);
-        } else {
-            xin[0] = load16(ip);
-            xin[1] = load16(ip + 1024);
-            xin[2] = load16(ip + 2048);
-            xin[3] = load16(ip + 3072);
-        }
+        const uint8_t* ip = src.in(j) + (su * job.in_sstride + unit_off(cu) + lane * 16u);
+        xin[0] = load16(ip);
+        xin[1] = load16(ip + 1024);
+        xin[2] = load16(ip + 2048);
+        xin[3] = load16(ip + 3072);
     };
     uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
-    if (builder && s < job.nstripes && bin < k) load_input(s, c, bin);
+    if (builder && s < job.nstripes && wave < k) load_input(s, c, wave);
     while (s < job.nstripes) {
         uint32_t s2 = s + job.gs_s, c2 = c + job.gs_c;  // this workgroup's next unit
         if (c2 >= job.cps) {
             c2 -= job.cps;
             ++s2;
         }
-        const uint64_t off = unit_off(s, c);
-        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        const uint64_t ob = s * job.out_sstride + unit_off(c) + lane * 16u;
         uint32_t acc[RT][2][8];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr)
@@ -886,32 +871,24 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
                 for (int b = 0; b < 8; ++b) acc[rr][g][b] = 0u;
         for (uint32_t f = 0; f < nph; ++f) {
             const uint32_t j0 = f * P;
-            // build: input j0 + bin (BB: its group bgrp) into slot bin
-            const uint32_t jb = j0 + bin;
+            // build: input j0 + wave into slot wave
+            const uint32_t jb = j0 + wave;
             if (builder && jb < k) {
-                char* slot = bsg_lds + bin * kBsgSlotBytes;
-                if constexpr (BB) {
-                    uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
-                    transpose8(g0);
-                    const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, h0[4] = {g0[4], g0[5], g0[6], g0[7]};
-                    write_combos1(slot, lane8 + 4u * bgrp, l0, 0u);
-                    write_combos1(slot, lane8 + 4u * bgrp, h0, 16u);
-                } else {
-                    uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
-                    uint32_t g1[8] = {xin[2].x, xin[2].y, xin[2].z, xin[2].w, xin[3].x, xin[3].y, xin[3].z, xin[3].w};
-                    transpose8(g0);
-                    transpose8(g1);
-                    const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, l1[4] = {g1[0], g1[1], g1[2], g1[3]};
-                    const uint32_t h0[4] = {g0[4], g0[5], g0[6], g0[7]}, h1[4] = {g1[4], g1[5], g1[6], g1[7]};
-                    write_combos(slot, lane8, l0, l1, 0u);
-                    write_combos(slot, lane8, h0, h1, 16u);
-                }
+                char* slot = bsg_lds + wave * kBsgSlotBytes;
+                uint32_t g0[8] = {xin[0].x, xin[0].y, xin[0].z, xin[0].w, xin[1].x, xin[1].y, xin[1].z, xin[1].w};
+                uint32_t g1[8] = {xin[2].x, xin[2].y, xin[2].z, xin[2].w, xin[3].x, xin[3].y, xin[3].z, xin[3].w};
+                transpose8(g0);
+                transpose8(g1);
+                const uint32_t l0[4] = {g0[0], g0[1], g0[2], g0[3]}, l1[4] = {g1[0], g1[1], g1[2], g1[3]};
+                const uint32_t h0[4] = {g0[4], g0[5], g0[6], g0[7]}, h1[4] = {g1[4], g1[5], g1[6], g1[7]};
+                write_combos(slot, lane8, l0, l1, 0u);
+                write_combos(slot, lane8, h0, h1, 16u);
             }
             if (builder) {  // prefetch: this unit's next phase, else the next unit's first
                 if (f + 1 < nph) {
                     if (jb + P < k) load_input(s, c, jb + P);
-                } else if (s2 < job.nstripes && bin < k) {
-                    load_input(s2, c2, bin);
+                } else if (s2 < job.nstripes && wave < k) {
+                    load_input(s2, c2, wave);
                 }
             }
             // this phase's coefficients (scalar loads, waited for before the barrier)
@@ -941,9 +918,6 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
                     acc[rr][0][b] = xor3(acc[rr][0][b], vl.x, vh.x);
                     acc[rr][1][b] = xor3(acc[rr][1][b], vl.y, vh.y);
                 }
-                // SB: one row's 16 LDS reads in flight at a time (hoisting the
-                // next rows' reads costs registers, i.e. occupancy)
-                if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
                 if (t + 1 < P * RT) {
 #pragma unroll
                     for (int b = 0; b < 16; ++b) o[b] = on[b];
@@ -957,7 +931,7 @@ __global__ __launch_bounds__(256) void matapply_bsg(const MatJob job) {
             if (i >= r) break;  // wave-uniform
             transpose8(acc[rr][0]);
             transpose8(acc[rr][1]);
-            uint8_t* op = kj->out[i] + ob;
+            uint8_t* op = src.out(i) + ob;
             store16_out<true>(op, u32x4{acc[rr][0][0], acc[rr][0][1], acc[rr][0][2], acc[rr][0][3]});
             store16_out<true>(op + 1024, u32x4{acc[rr][0][4], acc[rr][0][5], acc[rr][0][6], acc[rr][0][7]});
             store16_out<true>(op + 2048, u32x4{acc[rr][1][0], acc[rr][1][1], acc[rr][1][2], acc[rr][1][3]});
@@ -1048,14 +1022,8 @@ __global__ __launch_bounds__(kBlock) void matapply_small(const MatJob job) {
     }
 }
 
-// Launches whose unit kernels would run fewer lanes than this take
-// matapply_small (ZFEC_HIP_SMALL_LANES overrides, read per launch; 0 turns it
-// off).
-uint64_t small_lanes() {
-    const char* e = getenv("ZFEC_HIP_SMALL_LANES");
-    return e && *e ? strtoull(e, nullptr, 10) : 2048ull;
-}
-
+// Launches whose unit kernels would run fewer lanes than Config::small_lanes
+// (2048 by default) take matapply_small.
 hipError_t launch_small(MatJob& job, hipStream_t stream) {
     const uint32_t ub = job.sz >= 4 ? 4u : 1u;
     const uint64_t cps = (job.sz + ub - 1) / ub;
@@ -1066,7 +1034,6 @@ hipError_t launch_small(MatJob& job, hipStream_t stream) {
     job.cps = static_cast<uint32_t>(cps);
     job.gs_c = static_cast<uint32_t>(wpr);
     job.gs_s = ub;
-    job.xcd_swizzle = 0;
     const uint32_t grid = static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64));
     hipLaunchKernelGGL(matapply_small, dim3(grid), dim3(kBlock), 0, stream, job);
     return hipGetLastError();
@@ -1077,20 +1044,29 @@ hipError_t launch_small(MatJob& job, hipStream_t stream) {
 // ---------------------------------------------------------------------------
 typedef void (*KernelFn)(const MatJob);
 
-struct Variant {
-    KernelFn fn;
-    const char* name;
-    int max_blocks_per_cu;  // from the occupancy API, cached
-    bool kernarg_tables;    // the kernel reads job.tab[] instead of job.coef[]
-    int units_per_lane = 1; // units a lane handles per loop trip (grid sizing)
-    bool lds_tables = false; // dynamic LDS of 32 bytes per coefficient
-    int chunk = kChunk;      // bytes per unit (a lane's slice of one block)
-    int pad_tile = 0;        // kTilesPadded: rows per tile (the LDS table is padded to whole tiles)
-    bool rows = false;       // matapply_rows: one wave per stripe
-    KernelFn fn_wt = nullptr; // the same kernel with nt sc1 output stores (store_policy)
-};
+std::once_flag g_dispatch_once;
+int g_num_cu = 256;
+// Grid cap of the unit kernels: CUs x 8 x 1024 workgroups, i.e. about one unit
+// per lane for any launch this library makes (measured +9 % on 10^6 4 KiB
+// stripes against a grid of 16 resident waves per SIMD); a launch past it
+// walks grid-stride.
+constexpr uint64_t kGridPerCu = 8 * 1024;
 
-// Register-table variants: k <= 4, r <= 8.
+void init_dispatch() {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+            g_num_cu = prop.multiProcessorCount;
+    }
+}
+
+thread_local const char* t_last_kernel = "";
+thread_local uint32_t* t_signal_flag = nullptr;
+thread_local uint32_t t_signal_seq = 0;
+thread_local bool t_signal_used = false;
+
+// ---- register kernels (k <= 4, r <= 8) ----------------------------------------
 constexpr int kRegK = 4, kRegR = 8;
 const char* const kRegNames[kRegK + 1][kRegR + 1] = {
     {},
@@ -1102,42 +1078,28 @@ const char* const kRegNames[kRegK + 1][kRegR + 1] = {
      "matapply_reg<3,6>", "matapply_reg<3,7>", "matapply_reg<3,8>"},
     {"", "matapply_reg<4,1>", "matapply_reg<4,2>", "matapply_reg<4,3>", "matapply_reg<4,4>", "matapply_reg<4,5>",
      "matapply_reg<4,6>", "matapply_reg<4,7>", "matapply_reg<4,8>"}};
-Variant g_reg[kRegK + 1][kRegR + 1];
-Variant g_rows[kRegK + 1][kRegR + 1];
-char g_rows_names[kRegK + 1][kRegR + 1][24];
-Variant g_lds_fewin, g_lds_acc;
-// Padded-tile variants by tile height: 1-8 rows in one tile (r <= 8), 9-20
-// rows for wider codes split into ceil(r/20) near-equal tiles.
-constexpr int kMaxTile = 20;
-// Largest table: k = 32 inputs x (48 rows + up to 2 padding rows).
-constexpr int kMaxLdsTables = kMaxIn * (kMaxOut + 2);
-Variant g_lds_pad[kMaxTile + 1];
-std::once_flag g_dispatch_once;
-int g_num_cu = 0;
-int g_grid_mult = 1024;  // grid cap = CUs x resident blocks per CU x g_grid_mult (1024: ~one unit per lane; measured +9 % on 10^6 4 KiB stripes vs 16)
+const char* const kRowsNames[kRegK + 1][kRegR + 1] = {
+    {},
+    {"", "matapply_rows<1,1>", "matapply_rows<1,2>", "matapply_rows<1,3>", "matapply_rows<1,4>",
+     "matapply_rows<1,5>", "matapply_rows<1,6>", "matapply_rows<1,7>", "matapply_rows<1,8>"},
+    {"", "matapply_rows<2,1>", "matapply_rows<2,2>", "matapply_rows<2,3>", "matapply_rows<2,4>",
+     "matapply_rows<2,5>", "matapply_rows<2,6>", "matapply_rows<2,7>", "matapply_rows<2,8>"},
+    {"", "matapply_rows<3,1>", "matapply_rows<3,2>", "matapply_rows<3,3>", "matapply_rows<3,4>",
+     "matapply_rows<3,5>", "matapply_rows<3,6>", "matapply_rows<3,7>", "matapply_rows<3,8>"},
+    {"", "matapply_rows<4,1>", "matapply_rows<4,2>", "matapply_rows<4,3>", "matapply_rows<4,4>",
+     "matapply_rows<4,5>", "matapply_rows<4,6>", "matapply_rows<4,7>", "matapply_rows<4,8>"}};
 
-// Output store policy of the register kernels (ZFEC_HIP_STORE): "nt" streams
-// every store through the L2 write-back (nt); "ntsc1" writes through the L2
-// at device scope (nt sc1); "auto" (default) takes nt sc1 for single-stripe
-// launches -- a few long rows, where it measured faster: the cfg2 64 MiB
-// K=3/M=10 stripe, encode 68.5 -> 69.1-69.9 % of HBM from cold caches,
-// secondary decode 65.6 -> 68.0 %, bench value +1.2-1.5 % -- and nt for
+// Output store policy of the register kernels (Config::store, ZFEC_HIP_STORE):
+// "nt" streams every store through the L2 write-back (nt); "ntsc1" writes
+// through the L2 at device scope (nt sc1); "auto" (default) takes nt sc1 for
+// single-stripe launches -- a few long rows, where it measured faster: the
+// cfg2 64 MiB K=3/M=10 stripe, encode 68.5 -> 69.1-69.9 % of HBM from cold
+// caches, secondary decode 65.6 -> 68.0 %, bench value +1.2-1.5 % -- and nt for
 // batches of many stripes, where nt sc1 measured slower (256 x 1 MiB
 // object-major 69.5 -> 67.7 %, 10^6 x 4 KiB -1 %; tools/ab_store.sh,
 // profiles/r02_store_ab.log; copy-walk probe: tools/mb_cold.exe tail).
-enum StorePolicy { kStoreNt = 0, kStoreNtSc1 = 1, kStoreAuto = 2 };
-StorePolicy store_policy() {
-    static const StorePolicy p = [] {
-        const char* e = getenv("ZFEC_HIP_STORE");
-        if (e && !strcmp(e, "nt")) return kStoreNt;
-        if (e && !strcmp(e, "ntsc1")) return kStoreNtSc1;
-        return kStoreAuto;
-    }();
-    return p;
-}
-
 template <int K, int R>
-void set_reg() {
+hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
     // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
     // tools/mb_encode.exe; no gain for the 3-row decode)
     constexpr bool kPrefetch = R >= 5;
@@ -1145,176 +1107,313 @@ void set_reg() {
     // where they are used (K=3/M=10 encode 35.9 -> 33.6 us, tools/mb_encode.exe
     // variant "PF AL"; the 3-row decode is unchanged either way)
     constexpr bool kArgLoad = K * R * 5 >= 50;
-    g_reg[K][R] = Variant{matapply_reg<K, R, true, 1, 0, kPrefetch, 0, kArgLoad>, kRegNames[K][R], 0, true};
-    g_reg[K][R].fn_wt = matapply_reg<K, R, true, 1, 3, kPrefetch, 0, kArgLoad>;
-    snprintf(g_rows_names[K][R], sizeof g_rows_names[K][R], "matapply_rows<%d,%d>", K, R);
-    // the row walk loads every piece of a lane's share of the stripe before
-    // computing any (cfg5 encode 67.7 -> 70.1 % of HBM cold, decode 66.7 -> 69.8 %,
-    // tools/ab_store.sh, profiles/r02_rows_pre_ab.log); ZFEC_HIP_ROWS_PRE=0: one
-    // piece at a time (A/B)
-    static const bool rows_pre = [] {
-        const char* e = getenv("ZFEC_HIP_ROWS_PRE");
-        return !(e && e[0] == '0');
-    }();
-    g_rows[K][R] = Variant{rows_pre ? matapply_rows<K, R, kArgLoad, true> : matapply_rows<K, R, kArgLoad>,
-                           g_rows_names[K][R], 0, true};
-    g_rows[K][R].rows = true;
+    RegJob<K, R> job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.done_flag = nullptr;
+    job.done_seq = 0;
+    job.pad_ = 0;
+    for (int j = 0; j < K; ++j) job.in[j] = a.in[j];
+    for (int i = 0; i < R; ++i) job.out[i] = a.out[i];
+    for (int i = 0; i < R; ++i)
+        for (int j = 0; j < K; ++j) {
+            const uint32_t* w = &kHostBank.w[uint32_t(a.coef[size_t(i) * a.coef_stride + j]) * 8];
+            uint32_t* t = &job.tab[(i * K + j) * 5];
+            t[0] = w[0];
+            t[1] = w[1];
+            t[2] = w[2];
+            t[3] = w[3];
+            t[4] = w[4];
+        }
+    const bool rows = a.sz > kRowsMin && a.sz <= kRowsMax && a.nstripes >= 64;
+    const uint64_t cps = (a.sz + kChunk - 1) / kChunk;
+    if (cps * a.nstripes >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits
+    job.cps = static_cast<uint32_t>(cps);
+    // one unit per lane up to the grid cap; beyond it a grid-stride loop
+    const uint64_t lanes = rows ? a.nstripes * 64u : cps * a.nstripes;  // rows: one wave per stripe
+    const uint64_t need = (lanes + kBlock - 1) / kBlock;
+    const uint64_t cap = uint64_t(g_num_cu) * kGridPerCu;
+    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+    const uint64_t gstride = uint64_t(grid) * kBlock;
+    job.gs_s = static_cast<uint32_t>(gstride / cps);
+    job.gs_c = static_cast<uint32_t>(gstride % cps);
+    void (*fn)(const RegJob<K, R>);
+    const StorePolicy sp = config().store;
+    if (rows) {
+        fn = matapply_rows<K, R, kArgLoad>;
+        t_last_kernel = kRowsNames[K][R];
+    } else {
+        fn = (sp == kStoreNtSc1 || (sp == kStoreAuto && a.nstripes == 1)) ? matapply_reg<K, R, 3, kPrefetch, kArgLoad>
+                                                                            : matapply_reg<K, R, 0, kPrefetch, kArgLoad>;
+        t_last_kernel = kRegNames[K][R];
+        if (sig && grid == 1) {  // one workgroup: it signals its own completion
+            job.done_flag = sig;
+            job.done_seq = t_signal_seq;
+            t_signal_used = true;
+        }
+    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, stream, job);
+    return hipGetLastError();
 }
 
-template <int K>
-void fill_reg_row() {
-    set_reg<K, 1>();
-    set_reg<K, 2>();
-    set_reg<K, 3>();
-    set_reg<K, 4>();
-    set_reg<K, 5>();
-    set_reg<K, 6>();
-    set_reg<K, 7>();
-    set_reg<K, 8>();
+typedef hipError_t (*RegLaunch)(const ApplySpec&, hipStream_t, uint32_t*);
+
+template <int K, int... R>
+constexpr std::array<RegLaunch, kRegR + 1> reg_row(std::integer_sequence<int, R...>) {
+    return {{nullptr, launch_reg<K, R + 1>...}};
 }
+
+const std::array<RegLaunch, kRegR + 1> g_reg_launch[kRegK + 1] = {
+    {}, reg_row<1>(std::make_integer_sequence<int, kRegR>()), reg_row<2>(std::make_integer_sequence<int, kRegR>()),
+    reg_row<3>(std::make_integer_sequence<int, kRegR>()), reg_row<4>(std::make_integer_sequence<int, kRegR>())};
+
+// ---- table kernels (matapply_lds, k <= 32, r <= 48) ----------------------------
+struct LdsVariant {
+    KernelFn fn;
+    const char* name;
+    int chunk;     // bytes per unit (a lane's slice of one block)
+    int pad_tile;  // kTilesPadded: rows per tile (the LDS table is padded to whole tiles); 0: ragged
+};
+
+// Padded-tile variants by tile height: 1-8 rows in one tile (r <= 8), 9-20
+// rows for wider codes split into ceil(r/20) near-equal tiles.
+constexpr int kMaxTile = 20;
+char g_pad_names[kMaxTile + 1][40];
+LdsVariant g_lds_pad[kMaxTile + 1];
+// measured (tools/mb_encode.exe MB_AB, interleaved medians): k <= 4
+// (memory-bound) takes 16 bytes per lane in ragged 8-row tiles; wider codes
+// take 8 bytes per lane in padded tiles (no per-row branches), as few tiles as
+// 20-row register tiles allow (inputs are re-read per tile)
+const LdsVariant g_lds_fewin{matapply_lds<false, true, 8, 4, 4>, "matapply_lds<8,4,4>", 16, 0};
+const LdsVariant g_lds_acc{matapply_lds<true, false, 16, 2, 2>, "matapply_lds<16,2,2,acc>", 8, 0};
 
 template <int RT>
 void fill_pad() {
-    static char name[40];
     constexpr int G = (RT <= 4 || RT == 8) ? 4 : 2;  // input group size: measured per tile height
-    snprintf(name, sizeof name, "matapply_lds<%d,2,%d,pad>", RT, G);
-    g_lds_pad[RT] = Variant{matapply_lds<false, true, RT, 2, G, kTilesPadded>, name, 0, false, 1, true, 8, RT};
+    snprintf(g_pad_names[RT], sizeof g_pad_names[RT], "matapply_lds<%d,2,%d,pad>", RT, G);
+    g_lds_pad[RT] = LdsVariant{matapply_lds<false, true, RT, 2, G, kTilesPadded>, g_pad_names[RT], 8, RT};
     if constexpr (RT < kMaxTile) fill_pad<RT + 1>();
 }
 
-void init_dispatch() {
-    fill_reg_row<1>();
-    fill_reg_row<2>();
-    fill_reg_row<3>();
-    fill_reg_row<4>();
-    // measured (tools/mb_encode.exe MB_AB, interleaved medians): k <= 4
-    // (memory-bound) takes 16 bytes per lane in ragged 8-row tiles; wider
-    // codes take 8 bytes per lane in padded tiles (no per-row branches), as
-    // few tiles as 20-row register tiles allow (inputs are re-read per tile)
-    g_lds_fewin = Variant{matapply_lds<false, true, 8, 4, 4>, "matapply_lds<8,4,4>", 0, false, 1, true, 16};
-    g_lds_acc = Variant{matapply_lds<true, false, 16, 2, 2>, "matapply_lds<16,2,2,acc>", 0, false, 1, true, 8};
-    fill_pad<1>();
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) g_num_cu = prop.multiProcessorCount;
-    }
-    if (g_num_cu <= 0) g_num_cu = 256;
-    if (const char* e = getenv("ZFEC_HIP_GRID_MULT")) g_grid_mult = atoi(e) > 0 ? atoi(e) : g_grid_mult;
-}
+std::once_flag g_pad_once;
 
-// sz / nstripes: the launch's shape (0: the variant for long blocks)
-Variant* pick(uint32_t k, uint32_t r, bool acc, uint64_t sz = 0, uint64_t nstripes = 0) {
-    std::call_once(g_dispatch_once, init_dispatch);
-    if (acc) return &g_lds_acc;
-    if (k >= 1 && k <= static_cast<uint32_t>(kRegK) && r >= 1 && r <= static_cast<uint32_t>(kRegR)) {
-        if (sz > kRowsMin && sz <= kRowsMax && nstripes >= 64) return &g_rows[k][r];
-        return &g_reg[k][r];
-    }
-    if (k <= 4) return &g_lds_fewin;
+const LdsVariant& pick_lds(uint32_t k, uint32_t r, bool acc) {
+    std::call_once(g_pad_once, [] { fill_pad<1>(); });
+    if (acc) return g_lds_acc;
+    if (k <= 4) return g_lds_fewin;
     const uint32_t tiles = (r + kMaxTile - 1) / kMaxTile;
-    return &g_lds_pad[(r + tiles - 1) / tiles];
+    return g_lds_pad[(r + tiles - 1) / tiles];
 }
 
-thread_local const char* t_last_kernel = "";
-thread_local uint32_t* t_signal_flag = nullptr;
-thread_local uint32_t t_signal_seq = 0;
-thread_local bool t_signal_used = false;
+void fill_matjob(const ApplySpec& a, MatJob& job) {
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = a.k;
+    job.r = a.r;
+    job.cps = job.gs_c = job.gs_s = 0;
+    job.accumulate = a.accumulate;
+    job.pad_ = 0;
+    for (uint32_t j = 0; j < a.k; ++j) job.in[j] = a.in[j];
+    for (uint32_t i = 0; i < a.r; ++i) job.out[i] = a.out[i];
+}
+
+void fill_coef(const ApplySpec& a, MatJob& job) {
+    for (uint32_t i = 0; i < a.r; ++i) std::memcpy(&job.coef[i * a.k], a.coef + size_t(i) * a.coef_stride, a.k);
+}
+
+hipError_t launch_lds(const ApplySpec& a, hipStream_t stream) {
+    const LdsVariant& v = pick_lds(a.k, a.r, a.accumulate);
+    const uint64_t cps = (a.sz + v.chunk - 1) / v.chunk;
+    const uint64_t total = cps * a.nstripes;
+    if (total >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits larger jobs
+    MatJob job;
+    fill_matjob(a, job);
+    fill_coef(a, job);
+    job.cps = static_cast<uint32_t>(cps);
+    const size_t rows = v.pad_tile ? (a.r + v.pad_tile - 1) / v.pad_tile * v.pad_tile : a.r;
+    const size_t lds = size_t(a.k) * rows * 32;
+    const uint64_t need = (total + kBlock - 1) / kBlock;
+    const uint64_t cap = uint64_t(g_num_cu) * kGridPerCu;
+    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+    const uint64_t gstride = uint64_t(grid) * kBlock;
+    job.gs_s = static_cast<uint32_t>(gstride / cps);
+    job.gs_c = static_cast<uint32_t>(gstride % cps);
+    hipLaunchKernelGGL(v.fn, dim3(grid), dim3(kBlock), lds, stream, job);
+    t_last_kernel = v.name;
+    return hipGetLastError();
+}
 
 // ---- matapply_bsg dispatch ------------------------------------------------------
 // Rows per wave: the smallest instantiated RT >= ceil(r / 4).
 constexpr int kBsgRT[] = {1, 2, 3, 4, 5, 6, 8, 10, 12};
 constexpr int kBsgNumRT = sizeof(kBsgRT) / sizeof(kBsgRT[0]);
+constexpr uint32_t kBsgMaxRows = 4u * 12u;
 
 struct BsgVariant {
-    KernelFn fn = nullptr;
-    char name[40] = "";
-    int blocks_per_cu = 0;
-    int phase = 4;
+    const void* fn_karg = nullptr;  // matapply_bsg<RT, false, MatJob>
+    const void* fn_tbl = nullptr;   // matapply_bsg<RT, true, BsgTblJob>
+    char name[32] = "";
+    char name_tbl[32] = "";
+    int blocks_per_cu = 1;          // resident workgroups per CU (occupancy API), set once
 };
-// [0: P = 4, 1: P = 2, 2: P = 2 without the per-row sched_barrier, 3: as 2 with the balanced build][RT index]
-BsgVariant g_bsg_var[4][kBsgNumRT];
+BsgVariant g_bsg_var[kBsgNumRT];
 std::once_flag g_bsg_once;
 std::atomic<int> g_generic{-1};
 
-template <int I, int P, bool SB, bool BB = false>
+template <int I>
 void fill_bsg() {
     constexpr int RT = kBsgRT[I];
-    BsgVariant& v = g_bsg_var[P == 4 ? 0 : BB ? 3 : (SB ? 1 : 2)][I];
-    v.fn = matapply_bsg<RT, P, SB, BB>;
-    v.phase = P;
-    snprintf(v.name, sizeof v.name, BB ? "matapply_bsg<%d,%d,bb>" : SB ? "matapply_bsg<%d,%d>" : "matapply_bsg<%d,%d,nosb>",
-             RT, P);
-    if constexpr (I + 1 < kBsgNumRT) fill_bsg<I + 1, P, SB, BB>();
+    BsgVariant& v = g_bsg_var[I];
+    v.fn_karg = reinterpret_cast<const void*>(matapply_bsg<RT, false, MatJob>);
+    v.fn_tbl = reinterpret_cast<const void*>(matapply_bsg<RT, true, BsgTblJob>);
+    snprintf(v.name, sizeof v.name, "matapply_bsg<%d,2>", RT);
+    snprintf(v.name_tbl, sizeof v.name_tbl, "matapply_bsg<%d,2,tbl>", RT);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, v.fn_karg, 256, kBsgPhase * kBsgSlotBytes) == hipSuccess &&
+        nb > 0)
+        v.blocks_per_cu = nb;
+    else
+        (void)hipGetLastError();
+    if constexpr (I + 1 < kBsgNumRT) fill_bsg<I + 1>();
 }
 
-void init_bsg() {
-    fill_bsg<0, 4, true>();
-    fill_bsg<0, 2, true>();
-    fill_bsg<0, 2, false>();
-    fill_bsg<0, 2, false, true>();
+bool bsg_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    return generic_mode() != 0 && sz >= kBsgChunk && k >= 1 && k <= static_cast<uint32_t>(kMaxWideIn) && r >= 1 &&
+           r <= kBsgMaxRows && k * r >= 24 && !(k <= 4 && r <= 8);
 }
 
-bool bsg_eligible(const MatJob& job) {
-    if (generic_mode() == 0 || job.accumulate || job.tables == 1 || job.sz < kBsgChunk) return false;
-    if (job.k * job.r < 24 || (job.k <= 4 && job.r <= 8)) return false;
-    return job.r <= 4u * static_cast<uint32_t>(kBsgRT[kBsgNumRT - 1]);
+// Device-side argument tables of wide matapply_bsg launches, per thread and
+// device: a ring of slots in device memory filled by stream-ordered copies
+// from a pinned mirror; a slot is reused once the event recorded after its
+// last launch has completed.
+struct TableRing {
+    static constexpr int kSlots = 8;
+    static constexpr size_t kSlotBytes = size_t(16) << 10;
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    hipEvent_t ev[kSlots] = {};
+    bool busy[kSlots] = {};
+    unsigned next = 0;
+};
+
+struct Rings {
+    std::unordered_map<int, TableRing> dev;
+    ~Rings() {
+        for (auto& kv : dev) {
+            int cur = 0;
+            if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(kv.first) != hipSuccess) continue;
+            TableRing& t = kv.second;
+            for (int i = 0; i < TableRing::kSlots; ++i)
+                if (t.ev[i]) (void)hipEventSynchronize(t.ev[i]), (void)hipEventDestroy(t.ev[i]);
+            if (t.dev) (void)hipFree(t.dev);
+            if (t.host) (void)hipHostFree(t.host);
+            (void)hipSetDevice(cur);
+        }
+    }
+};
+thread_local Rings t_rings;
+
+hipError_t ring_slot(TableRing** ring, unsigned* slot) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    TableRing& t = t_rings.dev[dev];
+    if (!t.dev) {
+        if ((e = hipMalloc(&t.dev, TableRing::kSlots * TableRing::kSlotBytes)) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&t.host, TableRing::kSlots * TableRing::kSlotBytes, hipHostMallocDefault)) !=
+            hipSuccess) {
+            (void)hipFree(t.dev);
+            t.dev = nullptr;
+            return e;
+        }
+        for (int i = 0; i < TableRing::kSlots; ++i)
+            if ((e = hipEventCreateWithFlags(&t.ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    const unsigned s = t.next++ % TableRing::kSlots;
+    if (t.busy[s] && (e = hipEventSynchronize(t.ev[s])) != hipSuccess) return e;  // its last launch has read it
+    t.busy[s] = false;
+    *ring = &t;
+    *slot = s;
+    return hipSuccess;
 }
 
-hipError_t launch_bsg(MatJob& job, hipStream_t stream) {
-    std::call_once(g_dispatch_once, init_dispatch);
-    std::call_once(g_bsg_once, init_bsg);
-    const uint32_t need_rt = (job.r + 3) / 4;
+hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
+    std::call_once(g_bsg_once, [] { fill_bsg<0>(); });
+    const uint32_t k = a.k, r = a.r;
+    const uint32_t need_rt = (r + 3) / 4;
     int ri = 0;
     while (kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
-    // inputs per LDS phase: 2 (default: 32 KiB per workgroup, 4 workgroups per
-    // CU) or 4 (ZFEC_HIP_BSG_PHASE=4, A/B: 64 KiB, 2 per CU)
-    // (ZFEC_HIP_BSG_SB=1, A/B: a scheduling barrier after each row; without
-    // it the compiler overlaps rows and uses fewer registers: cfg4 decode
-    // 1679 -> 1842 GB/s of input, profiles/r02_bsg_ab.log)
-    // (ZFEC_HIP_BSG_BB=1, A/B: the input build balanced over all 4 waves)
-    const char* ph = getenv("ZFEC_HIP_BSG_PHASE");
-    const char* sb = getenv("ZFEC_HIP_BSG_SB");
-    const char* bb = getenv("ZFEC_HIP_BSG_BB");
-    BsgVariant& v =
-        g_bsg_var[(ph && ph[0] == '4') ? 0 : (sb && sb[0] == '1') ? 1 : (bb && bb[0] == '1') ? 3 : 2][ri];
+    const BsgVariant& v = g_bsg_var[ri];
     // coefficients in the kernel's walk order: wave w's bytes of phase f at
-    // (w * nph + f) * PB, (js, rr) in order: row w + 4 * rr of input P * f + js
-    const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = static_cast<uint32_t>(v.phase);
-    const uint32_t PB = (P * RT + 3) / 4 * 4, nph = (job.k + P - 1) / P;
-    if (4u * nph * PB > static_cast<uint32_t>(kMaxCoef)) return hipErrorNotSupported;
-    if (job.tables != 2) {
-        uint8_t cf[kMaxCoef] = {};
+    // (w * nph + f) * PB, (js, rr) in order: row w + 4 * rr of input 2 * f + js
+    const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = kBsgPhase;
+    const uint32_t PB = (P * RT + 3) / 4 * 4, nph = (k + P - 1) / P;
+    const uint32_t walk = 4u * nph * PB;
+    auto fill_walk = [&](uint8_t* cf) {
+        std::memset(cf, 0, walk);
         for (uint32_t w = 0; w < 4; ++w)
             for (uint32_t f = 0; f < nph; ++f)
                 for (uint32_t js = 0; js < P; ++js)
                     for (uint32_t rr = 0; rr < RT; ++rr) {
                         const uint32_t i = w + 4 * rr, j = P * f + js;
-                        cf[(w * nph + f) * PB + js * RT + rr] = i < job.r && j < job.k ? job.coef[i * job.k + j] : 0;
+                        if (i < r && j < k) cf[(w * nph + f) * PB + js * RT + rr] = a.coef[size_t(i) * a.coef_stride + j];
                     }
-        std::memcpy(job.coef, cf, sizeof cf);
-    }
-    job.tables = 2;  // idempotent: a relaunch of this job keeps the layout
-    const size_t lds = size_t(v.phase) * kBsgSlotBytes;
-    const uint64_t cps = (job.sz + kBsgChunk - 1) / kBsgChunk;
-    const uint64_t units = cps * job.nstripes;
+    };
+    const size_t lds = size_t(P) * kBsgSlotBytes;
+    const uint64_t cps = (a.sz + kBsgChunk - 1) / kBsgChunk;
+    const uint64_t units = cps * a.nstripes;
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
-    if (v.blocks_per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v.fn), 256, lds) !=
-                hipSuccess ||
-            nb <= 0)
-            nb = 1;
-        v.blocks_per_cu = nb;
-    }
     const uint64_t cap = uint64_t(g_num_cu) * v.blocks_per_cu * 8;
     const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    const uint32_t gs_s = static_cast<uint32_t>(grid / cps), gs_c = static_cast<uint32_t>(grid % cps);
+    if (k <= static_cast<uint32_t>(kMaxIn) && walk <= static_cast<uint32_t>(kMaxCoef)) {
+        MatJob job;
+        fill_matjob(a, job);
+        fill_walk(job.coef);
+        job.cps = static_cast<uint32_t>(cps);
+        job.gs_s = gs_s;
+        job.gs_c = gs_c;
+        hipLaunchKernelGGL(reinterpret_cast<void (*)(const MatJob)>(const_cast<void*>(v.fn_karg)), dim3(grid),
+                           dim3(256), lds, stream, job);
+        t_last_kernel = v.name;
+        return hipGetLastError();
+    }
+    // wide: pointers and coefficients in a device-side table
+    const size_t bytes = 8 * size_t(k + r) + walk;
+    if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
+    TableRing* ring = nullptr;
+    unsigned slot = 0;
+    hipError_t e = ring_slot(&ring, &slot);
+    if (e != hipSuccess) return e;
+    uint8_t* h = ring->host + slot * TableRing::kSlotBytes;
+    uint8_t* d = ring->dev + slot * TableRing::kSlotBytes;
+    std::memcpy(h, a.in, 8 * size_t(k));
+    std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
+    fill_walk(h + 8 * size_t(k + r));
+    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    BsgTblJob job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = k;
+    job.r = r;
     job.cps = static_cast<uint32_t>(cps);
-    job.gs_s = static_cast<uint32_t>(grid / cps);
-    job.gs_c = static_cast<uint32_t>(grid % cps);
-    hipLaunchKernelGGL(v.fn, dim3(grid), dim3(256), lds, stream, job);
-    t_last_kernel = v.name;
-    return hipGetLastError();
+    job.gs_s = gs_s;
+    job.gs_c = gs_c;
+    job.pad0_ = job.pad1_ = 0;
+    job.table = d;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(const BsgTblJob)>(const_cast<void*>(v.fn_tbl)), dim3(grid),
+                       dim3(256), lds, stream, job);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
+    ring->busy[slot] = true;
+    t_last_kernel = v.name_tbl;
+    return hipSuccess;
 }
 
 }  // namespace
@@ -1324,7 +1423,8 @@ int generic_mode() {
     if (g < 0) {
         const char* e = getenv("ZFEC_HIP_GENERIC");
         g = (e && e[0] == '0') ? 0 : 1;
-        g_generic.store(g);
+        int expect = -1;
+        if (!g_generic.compare_exchange_strong(expect, g)) g = expect;  // set_generic_mode won the race
     }
     return g;
 }
@@ -1332,7 +1432,9 @@ int generic_mode() {
 void set_generic_mode(int on) { g_generic.store(on ? 1 : 0); }
 
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate) {
-    return pick(k, r, accumulate)->name;
+    if (!accumulate && k >= 1 && k <= static_cast<uint32_t>(kRegK) && r >= 1 && r <= static_cast<uint32_t>(kRegR))
+        return kRegNames[k][r];
+    return pick_lds(k, r, accumulate).name;
 }
 
 const char* matapply_last_kernel() { return t_last_kernel; }
@@ -1344,86 +1446,51 @@ void matapply_request_signal(uint32_t* flag_dev, uint32_t seq) {
 
 bool matapply_signal_used() { return t_signal_used; }
 
-hipError_t launch_matapply(MatJob& job, hipStream_t stream) {
+bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    // matapply_bsg's table form, or (forced) a specialised kernel of the whole matrix
+    return bsg_shape_ok(k, r, sz) ||
+           (jit_mode() == kJitForce && sz >= static_cast<uint64_t>(kBsChunk) && k * r <= kJitMaxCoef);
+}
+
+hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     uint32_t* const sig = t_signal_flag;  // a request covers this launch only
     t_signal_flag = nullptr;
     t_signal_used = false;
-    job.done_flag = nullptr;
-    if (job.k == 0 || job.k > static_cast<uint32_t>(kMaxIn) || job.r == 0 || job.r > static_cast<uint32_t>(kMaxOut) ||
-        job.r * job.k > static_cast<uint32_t>(kMaxCoef) || job.nstripes == 0 || job.sz == 0)
+    std::call_once(g_dispatch_once, init_dispatch);
+    const uint32_t k = a.k, r = a.r;
+    if (k == 0 || r == 0 || a.nstripes == 0 || a.sz == 0 || a.nstripes >= (1ull << 32) || a.coef_stride < k ||
+        k > static_cast<uint32_t>(kMaxWideIn) || r > static_cast<uint32_t>(kMaxOut))
         return hipErrorInvalidValue;
-    if (!job.tables) {  // a run-time specialised bit-sliced kernel, where one applies and is compiled
+    const bool wide = k > static_cast<uint32_t>(kMaxIn);
+    if (!wide && k * r > static_cast<uint32_t>(kMaxCoef)) return hipErrorInvalidValue;
+    if (!a.accumulate) {  // a run-time specialised bit-sliced kernel, where one applies and is compiled
         const char* jit_name = nullptr;
-        const hipError_t je = launch_matapply_jit(job, stream, &jit_name);
+        const hipError_t je = launch_matapply_jit(a, stream, &jit_name);
         if (je == hipSuccess) {
             t_last_kernel = jit_name;
             return hipSuccess;
         }
         if (je != hipErrorNotSupported && je != hipErrorNotReady) return je;
     }
-    if (!job.tables && !(job.k <= static_cast<uint32_t>(kRegK) && job.r <= static_cast<uint32_t>(kRegR)) &&
-        (job.sz + 7) / 8 * job.nstripes < small_lanes()) {
+    const bool reg = k <= static_cast<uint32_t>(kRegK) && r <= static_cast<uint32_t>(kRegR);
+    if (wide) {
+        if (a.accumulate || !bsg_shape_ok(k, r, a.sz)) return hipErrorNotSupported;
+        return launch_bsg(a, stream);
+    }
+    const Config& cfg = config();
+    if (!reg && (a.sz + 7) / 8 * a.nstripes < cfg.small_lanes) {
+        MatJob job;
+        fill_matjob(a, job);
+        fill_coef(a, job);
         const hipError_t se = launch_small(job, stream);
         if (se != hipErrorNotSupported) {
             t_last_kernel = "matapply_small";
             return se;
         }
     }
-    if (bsg_eligible(job)) {
-        const hipError_t be = launch_bsg(job, stream);
-        if (be != hipErrorNotSupported) return be;  // else the table kernels serve
-    }
-    Variant* v = pick(job.k, job.r, job.accumulate != 0, job.sz, job.nstripes);
-    const uint64_t cps = (job.sz + v->chunk - 1) / v->chunk;
-    const uint64_t total = cps * job.nstripes;
-    if (total >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits larger jobs
-    job.cps = static_cast<uint32_t>(cps);
-
-    const size_t rows = v->pad_tile ? (job.r + v->pad_tile - 1) / v->pad_tile * v->pad_tile : job.r;
-    const size_t lds = v->lds_tables ? size_t(job.k) * rows * 32 : 0;
-    if (v->max_blocks_per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(v->fn), kBlock,
-                                                         v->lds_tables ? kMaxLdsTables * 32 : 0) !=
-                hipSuccess ||
-            nb <= 0)
-            nb = 1;
-        v->max_blocks_per_cu = nb;
-    }
-    // One unit per lane up to g_grid_mult x the resident capacity; beyond that
-    // a grid-stride loop.
-    const uint64_t lanes = v->rows ? uint64_t(job.nstripes) * 64u  // one wave per stripe
-                                   : (total + v->units_per_lane - 1) / v->units_per_lane;
-    const uint64_t need = (lanes + kBlock - 1) / kBlock;
-    const uint64_t cap = static_cast<uint64_t>(g_num_cu) * v->max_blocks_per_cu * g_grid_mult;
-    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
-    const uint64_t gstride = static_cast<uint64_t>(grid) * kBlock;
-    job.gs_s = static_cast<uint32_t>(gstride / cps);
-    job.gs_c = static_cast<uint32_t>(gstride % cps);
-    if (v->kernarg_tables && !job.tables) {  // idempotent: a job may be relaunched
-        uint8_t c[kMaxKernargTables];
-        const uint32_t n = job.k * job.r;
-        for (uint32_t i = 0; i < n; ++i) c[i] = job.coef[i];
-        for (uint32_t i = 0; i < n; ++i)
-            for (int q = 0; q < 5; ++q) job.tab[i * 5 + q] = kHostBank.w[c[i] * 8 + q];
-        job.tables = 1;
-    }
-    // XCD-contiguous order: off by default (ZFEC_HIP_XCD=1 for A/B runs;
-    // measured 2 % slower on 256 x 1 MiB K=3/M=10 encodes from cold caches,
-    // tools/mb_cold.hip, profiles/r02_mb_cold.log)
-    const char* xe = getenv("ZFEC_HIP_XCD");
-    job.xcd_swizzle = (xe && xe[0] == '1') && !v->rows;
-    KernelFn fn = v->fn;
-    if (v->fn_wt && (store_policy() == kStoreNtSc1 || (store_policy() == kStoreAuto && job.nstripes == 1)))
-        fn = v->fn_wt;
-    if (sig && v->fn_wt && grid == 1) {  // a register kernel (fn_wt: only they have one), one workgroup
-        job.done_flag = sig;
-        job.done_seq = t_signal_seq;
-        t_signal_used = true;
-    }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, stream, job);
-    t_last_kernel = v->name;
-    return hipGetLastError();
+    if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
+    if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
+    return launch_lds(a, stream);
 }
 
 }  // namespace zfec_hip

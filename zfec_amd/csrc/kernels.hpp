@@ -13,14 +13,32 @@
 
 namespace zfec_hip {
 
-constexpr int kMaxIn = 32;     // input blocks per launch (larger k: XOR-accumulating passes)
-constexpr int kMaxOut = 48;    // output blocks per launch
-constexpr int kMaxCoef = 1536; // r*k coefficients per launch
-constexpr int kChunk = 16;     // bytes per lane per block per step (one dwordx4)
-constexpr int kMinChunk = 4;   // smallest unit any kernel variant uses (launch splitting)
-constexpr int kBlock = 256;    // threads per workgroup
+constexpr int kMaxIn = 32;       // inputs per launch of the table / small kernels (wider: XOR-accumulating passes)
+constexpr int kMaxOut = 48;      // outputs per launch
+constexpr int kMaxCoef = 1536;   // r*k coefficients per launch of the table kernels
+constexpr int kMaxWideIn = 256;  // inputs per launch of the bit-sliced kernels (a device-side table past kMaxIn)
+constexpr int kChunk = 16;       // bytes per lane per block per step (one dwordx4)
+constexpr int kMinChunk = 4;     // smallest unit any kernel variant uses (launch splitting)
+constexpr int kBlock = 256;      // threads per workgroup
 
-// Kernel argument block (passed by value; ~2.2 KiB, well inside the kernarg limit).
+// One matrix application, as the host describes it (not a kernel argument:
+// every kernel family builds its own, sized to what it reads).
+struct ApplySpec {
+    const uint8_t* coef;          // r x k coefficients, row i at coef + i * coef_stride
+    uint32_t coef_stride;         // >= k
+    uint32_t k, r;
+    const uint8_t* const* in;     // k input block bases (stripe 0), kernel-visible addresses
+    uint8_t* const* out;          // r output block bases (stripe 0)
+    uint64_t sz;                  // bytes per block
+    uint64_t nstripes;
+    uint64_t in_sstride, out_sstride;  // stripe strides added to every input / output pointer
+    bool accumulate;              // out ^= result (continuation pass of a code split by input groups)
+};
+
+// Kernel argument block of the table (matapply_lds), small and run-time-data
+// bit-sliced (matapply_bsg) kernels: ~2.2 KiB, k <= kMaxIn, r <= kMaxOut.
+// The register kernels (k <= 4, r <= 8) take a block sized to k + r pointers
+// and their tables instead (kernels.hip, RegJob).
 struct alignas(16) MatJob {
     uint64_t sz;           // bytes per block
     uint64_t in_sstride;   // stripe stride added to every input pointer
@@ -28,39 +46,33 @@ struct alignas(16) MatJob {
     uint32_t nstripes;
     uint32_t k;            // inputs in this launch
     uint32_t r;            // outputs in this launch
-    uint32_t cps;          // 16-byte chunks per stripe = ceil(sz / 16)
-    uint32_t gs_c, gs_s;   // grid stride expressed as (chunks, stripes): stride = gs_s*cps + gs_c
-    uint32_t accumulate;   // 1: out ^= result (continuation pass for k > kMaxIn)
-    uint32_t tables;       // set by launch_matapply: 1 = tab[] holds the per-coefficient tables,
-                           // 2 = coef[] is in matapply_bsg's walk order
-    uint32_t xcd_swizzle;  // set by launch_matapply: 1 = workgroups dealt XCD-contiguously (UnitIter)
+    uint32_t cps;          // units per stripe
+    uint32_t gs_c, gs_s;   // grid stride expressed as (units, stripes): stride = gs_s*cps + gs_c
+    uint32_t accumulate;   // 1: out ^= result
     uint32_t pad_;
-    uint32_t* done_flag;   // set by launch_matapply: pinned host word the kernel's one workgroup
-    uint32_t done_seq;     //   stores done_seq into when it has finished (matapply_request_signal)
-    uint32_t pad2_;
     const uint8_t* in[kMaxIn];
     uint8_t* out[kMaxOut];
-    union {
-        uint8_t coef[kMaxCoef];          // r x k coefficients, row-major (filled by the caller)
-        uint32_t tab[kMaxCoef / 4];      // or their v_perm tables, 5 dwords each (filled by launch_matapply)
-    };
+    uint8_t coef[kMaxCoef];  // r x k row-major (matapply_bsg: its walk order)
 };
 
-constexpr int kMaxKernargTables = kMaxCoef / 4 / 5;  // 76 coefficients
+// Enqueue one launch on `stream` (the current device's).  Returns
+// hipErrorInvalidValue for shapes no kernel accepts (the caller splits),
+// hipErrorNotSupported when a wide launch (k > kMaxIn) has no kernel for its
+// shape (the caller splits it into XOR-accumulating passes).
+hipError_t launch_apply(const ApplySpec& a, hipStream_t stream);
 
-// Enqueue one launch on `stream`.  Validates shapes against the kernel's
-// compile-time limits before launching (returns hipErrorInvalidValue
-// otherwise); chooses the specialised variant for (k, r) when one exists.
-hipError_t launch_matapply(MatJob& job, hipStream_t stream);
+// Whether launch_apply takes all k > kMaxIn inputs of a launch of r <= kMaxOut
+// rows and sz-byte blocks in one pass (bit-sliced kernels).
+bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz);
 
-// Ask the calling thread's next launch_matapply to have its kernel publish
-// `seq` at flag_dev (pinned host memory) when it has finished -- honoured
-// only by the register kernels in a one-workgroup launch (a stripe of at
-// most 4 KiB per block); matapply_signal_used() says whether it was.
+// Ask the calling thread's next launch_apply to have its kernel publish `seq`
+// at flag_dev (pinned host memory) when it has finished -- honoured only by
+// the register kernels in a one-workgroup launch (a stripe of at most 4 KiB
+// per block); matapply_signal_used() says whether it was.
 void matapply_request_signal(uint32_t* flag_dev, uint32_t seq);
 bool matapply_signal_used();
 
-// Name of the table-kernel variant launch_matapply uses for (k, r) when no
+// Name of the table-kernel variant launch_apply uses for (k, r) when no
 // run-time specialised kernel applies (for tests / profiling).
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
 
