@@ -445,22 +445,36 @@ LEGS = Legs()
 COLD_SPAN = 768 << 20
 
 
+# GPU time of untimed launches before a back-to-back measurement: the chip
+# lowers its clock some milliseconds into sustained load and settles after
+# that (K=20/M=60 encode: 680-850 us per launch a few milliseconds in, 590 us
+# after 180 ms; tools/jit_probe.py), so the timed
+# launches start in the settled state
+WARM_MS = 200.0
+
+
 def back_to_back(fns, n, stream, leg):
     """Average GPU duration of n launches queued back to back, fns[i % len]
-    for launch i.  The stream is held by a spin kernel while the host enqueues
-    them, so the host's per-call cost cannot leave gaps between the timed
-    launches.  Returns (ms per launch, host enqueue us per launch)."""
+    for launch i, after untimed launches of the same kind worth WARM_MS of GPU
+    time (at most 2000).  The stream is held by a spin kernel while the host
+    starts enqueueing them, so the host's per-call cost cannot leave gaps
+    between the timed launches.  Returns (ms per launch, host enqueue us per
+    launch)."""
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
     fns[0](stream.cuda_stream)
+    b.record(stream)
     LEGS.add(leg + " (untimed)", capi.last_kernel_name())
+    torch.cuda.synchronize()
+    warm = int(min(2000, max(3, WARM_MS / max(1e-3, a.elapsed_time(b)))))
     torch.cuda._sleep(20_000_000)
-    for i in range(3):  # queued behind the spin kernel too: the timed launches start on a busy GPU
+    for i in range(warm):  # queued behind the spin kernel too: the timed launches start on a busy GPU
         fns[(i + 1) % len(fns)](stream.cuda_stream)
         LEGS.add(leg + " (untimed)", capi.last_kernel_name())
     a.record(stream)
     h0 = time.perf_counter()
     for i in range(n):
-        fns[(i + 4) % len(fns)](stream.cuda_stream)
+        fns[(i + 1 + warm) % len(fns)](stream.cuda_stream)
     host_us = (time.perf_counter() - h0) / n * 1e6
     b.record(stream)
     kern = capi.last_kernel_name()
@@ -787,12 +801,13 @@ def main():
     if args.slabs:
         desc = desc.replace("stripe per GPU", "stripe split into byte-range slabs across GPUs")
     row_padding = not args.no_row_padding
-    timing = ("%d launches back to back between two HIP events on the launch stream, enqueued (after 4 untimed "
-              "ones) while a spin kernel holds the stream (average launch duration, no host gaps), over a rotation "
+    timing = ("%d launches back to back between two HIP events on the launch stream, enqueued while a spin kernel "
+              "holds the stream (average launch duration, no host gaps) after untimed launches worth %.0f ms of GPU "
+              "time (the clock the chip settles at under sustained load), over a rotation "
               "of %d disjoint buffer sets spanning >= 768 MiB (3x the 256 MiB Infinity Cache), so every launch "
               "reads and writes HBM; *_warm: the same on one buffer set (as the timed loop runs); "
               "launch_ms_event_pairs: mean of %d encode/decode steps as in the timed loop with a HIP event pair "
-              "around each launch" % (t["b2b_launches"], t["nsets"], t["pair_launches"]))
+              "around each launch" % (t["b2b_launches"], WARM_MS, t["nsets"], t["pair_launches"]))
     out = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -144,6 +144,22 @@ def uint_array(vals):
     return (ctypes.c_uint * max(1, len(vals)))(*vals)
 
 
+_UINT_CACHE = {}
+
+
+def _nums(vals):
+    """uint_array(vals), cached per tuple of values: a batched call's block
+    numbers are usually the same every call (the ctypes array construction
+    is about a microsecond of the per-call host cost)."""
+    key = tuple(vals)
+    a = _UINT_CACHE.get(key)
+    if a is None:
+        if len(_UINT_CACHE) > 4096:
+            _UINT_CACHE.clear()
+        a = _UINT_CACHE[key] = uint_array(key)
+    return a
+
+
 class Code(object):
     """RAII wrapper around fec_t* (fec_new / fec_free)."""
 
@@ -169,12 +185,16 @@ class Code(object):
         check(lib().fec_jit_prepare_decode(self.ptr, uint_array(index), flags))
 
     def encode_batch(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
-        check(lib().fec_encode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(block_nums),
-                                     len(block_nums), sz, nstripes, stream or None, flags))
+        st = _lib.fec_encode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, _nums(block_nums), len(block_nums), sz,
+                                   nstripes, stream or None, flags)
+        if st:
+            check(st)
 
     def decode_batch(self, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
-        check(lib().fec_decode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, uint_array(index),
-                                     sz, nstripes, stream or None, flags))
+        st = _lib.fec_decode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, _nums(index), sz, nstripes,
+                                   stream or None, flags)
+        if st:
+            check(st)
 
     def encode_batch_multi(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, devices, flags=0):
         """fec_encode_batch_multi: the stripes split over `devices` (host memory)."""

@@ -186,6 +186,9 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
     e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", opt.store_aux, opt.shift64 ? 1 : 0);
     e.s += kPrelude;
+    if (opt.probe == 1)
+        e("__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs0(const u8* p) {\n"
+          "  return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(p), (short)0, 0, 0x00020000);\n}\n");
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
     // split: the row tiles of a unit go to the waves of one workgroup, which
     // read the unit's inputs at the same time (L1/L2 hits instead of a re-read
@@ -232,16 +235,13 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // share: each wave of the workgroup loads and transposes k / ntiles of the
     // unit's inputs once and leaves their bit-planes in LDS for all waves
     const bool share = split && opt.share;
-    // probe 1 (no HBM traffic): an input is synthesised from the lane, the
-    // unit and the block number instead of loaded
+    // probe 1 (no HBM traffic): every buffer resource gets num_records = 0,
+    // so each load returns zeros and each store is dropped by the address
+    // check -- the same instruction stream, no memory traffic
     const unsigned probe = opt.probe;
-    auto emit_ld = [&](const char* ind, const char* dst, const char* rsrc, unsigned j) {
-        if (probe == 1)
-            e("%sconst u32x4 %s_0 = u32x4{lo16 ^ (u32)ub, %uu, (u32)ub, lo16 + %uu}, %s_1 = u32x4{(u32)ub + %uu, lo16, "
-              "%uu ^ (u32)ub, lo16 * %uu};\n",
-              ind, dst, j * 2654435761u, j, dst, j * 40503u, j + 7, 2 * j + 1);
-        else
-            e("%sconst u32x4 %s_0 = ld(%s, lo16), %s_1 = ld(%s, lo16 + 1024u);\n", ind, dst, rsrc, dst, rsrc);
+    const char* const RS = probe == 1 ? "rs0" : "rs";
+    auto emit_ld = [&](const char* ind, const char* dst, const char* rsrc, unsigned) {
+        e("%sconst u32x4 %s_0 = ld(%s, lo16), %s_1 = ld(%s, lo16 + 1024u);\n", ind, dst, rsrc, dst, rsrc);
     };
     auto emit_load = [&](unsigned n) {
         const unsigned j = n % k;
@@ -252,7 +252,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         char dst[16], rsrc[16];
         snprintf(dst, sizeof dst, "l%u", n);
         snprintf(rsrc, sizeof rsrc, "ri%u", n);
-        if (probe != 1) e("    const __amdgpu_buffer_rsrc_t ri%u = rs(%sin[%u] + ub);\n", n, PA, j);
+        e("    const __amdgpu_buffer_rsrc_t ri%u = %s(%sin[%u] + ub);\n", n, RS, PA, j);
         emit_ld("    ", dst, rsrc, j);
     };
     if (!split)
@@ -267,7 +267,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                 char dst[16], rsrc[16];
                 snprintf(dst, sizeof dst, "p%u", j);
                 snprintf(rsrc, sizeof rsrc, "pi%u", j);
-                if (probe != 1) e("      const __amdgpu_buffer_rsrc_t pi%u = rs(%sin[%u] + ub);\n", j, PA, j);
+                e("      const __amdgpu_buffer_rsrc_t pi%u = %s(%sin[%u] + ub);\n", j, RS, PA, j);
                 emit_ld("      ", dst, rsrc, j);
             }
             for (unsigned j = t; j < k; j += ntiles) {
@@ -390,12 +390,9 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             }
             if (probe != 2)
                 e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
-            const char* guard = probe == 1 ? "    if (a%u_0 == 0x9E3779B9u && a%u_5 == 0x7F4A7C15u) {\n" : nullptr;
-            if (guard) e(guard, i, i);
-            e("    const __amdgpu_buffer_rsrc_t ro%u = rs(%sout[%u] + uo);\n", i, PA, i);
+            e("    const __amdgpu_buffer_rsrc_t ro%u = %s(%sout[%u] + uo);\n", i, RS, PA, i);
             e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
             e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
-            if (guard) e("    }\n");
         }
         if (split) e("    }\n");
     }
@@ -845,7 +842,7 @@ hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const cha
     for (unsigned i = 0; i < r; ++i) args[5 + k + i] = reinterpret_cast<uint64_t>(a.out[i]);
     size_t size = (5 + k + r) * sizeof(uint64_t);
     void* conf[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, 0, stream, nullptr, conf);
+    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, cfg->jit_lds, stream, nullptr, conf);
     if (er == hipSuccess && name_out) *name_out = name;
     return er;
 }

@@ -24,6 +24,7 @@ struct Config {
     StorePolicy store;     // ZFEC_HIP_STORE=auto|nt|ntsc1: output store policy of the register kernels
     uint64_t small_lanes;  // ZFEC_HIP_SMALL_LANES: launches below this many lanes take matapply_small (0: never)
     BsOptions jit;         // ZFEC_HIP_JIT_*: code-generation options of the bit-sliced JIT kernels
+    unsigned jit_lds;      // ZFEC_HIP_JIT_LDS: extra dynamic LDS bytes per JIT workgroup (A/B: caps residency)
     // host paths
     bool wait_signal;      // ZFEC_HIP_WAIT=sync: small calls wait in hipStreamSynchronize
     size_t pack_limit;     // ZFEC_HIP_PACK_LIMIT: host bytes a call packs into the bounce buffer

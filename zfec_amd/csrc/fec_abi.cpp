@@ -305,7 +305,8 @@ int apply_matrix_range(const uint8_t* coef, unsigned coef_stride, unsigned k, un
     const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
     const size_t stripes_per_launch = std::max<size_t>(1, config().launch_units / cps);
     // wide codes: every input in one bit-sliced pass per row group
-    const bool wide = k > static_cast<unsigned>(kMaxIn) && wide_launch_ok(k, std::min<unsigned>(r, kMaxOut), sz);
+    const bool wide = k > static_cast<unsigned>(kMaxIn) &&
+                      wide_launch_ok(k, std::min<unsigned>(r, kMaxOut), sz, std::min(stripes_per_launch, nstripes));
     const unsigned kstep = wide ? k : static_cast<unsigned>(kMaxIn);
     const uint8_t* pin[kMaxWideIn];
     uint8_t* pout[kMaxWideIn];

@@ -1446,10 +1446,14 @@ void matapply_request_signal(uint32_t* flag_dev, uint32_t seq) {
 
 bool matapply_signal_used() { return t_signal_used; }
 
-bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz) {
-    // matapply_bsg's table form, or (forced) a specialised kernel of the whole matrix
-    return bsg_shape_ok(k, r, sz) ||
-           (jit_mode() == kJitForce && sz >= static_cast<uint64_t>(kBsChunk) && k * r <= kJitMaxCoef);
+bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes) {
+    // (forced) a specialised kernel of the whole matrix
+    if (jit_mode() == kJitForce && sz >= static_cast<uint64_t>(kBsChunk) && k * r <= kJitMaxCoef) return true;
+    // launches too small to fill the chip: matapply_small's passes of 32 inputs
+    // (a wave per output row, every input load in flight at once) beat one
+    // matapply_bsg launch walking all inputs in phases of 2
+    if ((sz + 7) / 8 * nstripes < config().small_lanes) return false;
+    return bsg_shape_ok(k, r, sz);  // matapply_bsg's table form
 }
 
 hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {

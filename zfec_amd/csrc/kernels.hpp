@@ -62,8 +62,8 @@ struct alignas(16) MatJob {
 hipError_t launch_apply(const ApplySpec& a, hipStream_t stream);
 
 // Whether launch_apply takes all k > kMaxIn inputs of a launch of r <= kMaxOut
-// rows and sz-byte blocks in one pass (bit-sliced kernels).
-bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz);
+// rows, sz-byte blocks and nstripes stripes in one pass (bit-sliced kernels).
+bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes);
 
 // Ask the calling thread's next launch_apply to have its kernel publish `seq`
 // at flag_dev (pinned host memory) when it has finished -- honoured only by

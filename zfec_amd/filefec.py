@@ -393,15 +393,19 @@ def _segments(inf, k, m, chunksize):
     offset of its parity) per full segment in file order, then
     (tail bytes, None, None, None) once for the final short segment -- empty
     when the file is a whole number of segments, as the reference's loops
-    (filefec.py:352-375, :473-492) also end on a segment they pad entirely."""
+    (filefec.py:352-375, :473-492) also end on a segment they pad entirely.
+    The window starts at 4 segments and doubles up to WINDOW_BYTES, so a slow
+    stream (a pipe, a socket) sees its first callbacks after a few segments,
+    as with the reference's segment-at-a-time loop, not after 64 MiB."""
     seg = k * chunksize
     r = m - k
     wseg = max(1, WINDOW_BYTES // seg)
     code = capi.Code(k, m)
     win_in, rows = _PinnedArray(wseg * seg), _PinnedArray(max(1, r) * wseg * chunksize)
+    cur = min(wseg, 4)
     try:
         while True:
-            got = _readinto_full(inf, memoryview(win_in.array)[:wseg * seg])
+            got = _readinto_full(inf, memoryview(win_in.array)[:cur * seg])
             nfull = got // seg
             if nfull and r:
                 code.encode_batch(win_in.ptr, chunksize, seg, rows.ptr, chunksize, r * chunksize, list(range(k, m)),
@@ -410,9 +414,10 @@ def _segments(inf, k, m, chunksize):
             par = rows.array[:nfull * r * chunksize].tobytes()
             for s in range(nfull):
                 yield win, s * seg, par, s * r * chunksize
-            if got < wseg * seg:
+            if got < cur * seg:
                 yield bytes(win_in.array[nfull * seg:got]), None, None, None
                 return
+            cur = min(wseg, 2 * cur)
     finally:
         win_in.free()
         rows.free()
