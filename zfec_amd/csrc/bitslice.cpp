@@ -173,8 +173,129 @@ bool bitslice_split(unsigned r, const BsOptions& opt) {
     return opt.split && nt > 1 && nt <= 8;
 }
 
+bool bitslice_ksplit(unsigned k, unsigned r, const BsOptions& opt) {
+    return opt.ksplit && k > 32 && bitslice_tiles(r, opt) == 1 && r <= 10;
+}
+
+namespace {
+// The updates of one input step n (input j) to the accumulators of rows
+// [r0, r1): acc ^= L[lo] ^ H[hi] per output plane (shared by both generators).
+void emit_updates(Src& e, const std::vector<uint8_t>& masks, unsigned k, unsigned j, unsigned n, unsigned r0,
+                  unsigned r1, std::vector<char>& init) {
+    Combos lo{n, 'L', 0}, hi{n, 'H', 4};
+    for (unsigned i = r0; i < r1; ++i) {
+        const uint8_t* mk = &masks[(size_t(i) * k + j) * 8];
+        for (unsigned b = 0; b < 8; ++b) {
+            if (!mk[b]) continue;
+            const unsigned ml = mk[b] & 15u, mh = unsigned(mk[b]) >> 4;
+            const std::string sl = ml ? lo.name(ml, e) : std::string(), sh = mh ? hi.name(mh, e) : std::string();
+            char acc[32];
+            snprintf(acc, sizeof acc, "a%u_%u", i, b);
+            char& ini = init[size_t(i - r0) * 8 + b];
+            if (!ini) {
+                if (ml && mh)
+                    e("    %s = %s ^ %s;\n", acc, sl.c_str(), sh.c_str());
+                else
+                    e("    %s = %s;\n", acc, ml ? sl.c_str() : sh.c_str());
+                ini = 1;
+            } else if (ml && mh) {
+                e("    %s = x3(%s, %s, %s);\n", acc, acc, sl.c_str(), sh.c_str());
+            } else {
+                e("    %s ^= %s;\n", acc, ml ? sl.c_str() : sh.c_str());
+            }
+        }
+    }
+}
+
+// Wide codes with one row tile (k > 32, r <= 10; e.g. 94/100): the unit's
+// inputs are split over the 4 waves of a workgroup (wave w: inputs
+// [w*k/4, (w+1)*k/4)), each wave accumulates the partial planes of every row
+// from its inputs, the partials go through LDS, and wave w reduces, transposes
+// and stores rows w, w+4, ...  A 64 MiB stripe of 94/100 has 349 units of
+// 2 KiB: one wave per unit leaves most of the chip idle, four per unit do not.
+std::string source_ksplit(const std::vector<uint8_t>& masks, unsigned k, unsigned r, const BsOptions& opt,
+                          const char* name) {
+    Src e;
+    e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
+    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", opt.store_aux, opt.shift64 ? 1 : 0);
+    e.s += kPrelude;
+    e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
+    e("extern \"C\" __global__ __launch_bounds__(256) void %s(const Args a) {\n", name);
+    e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n  const u32 lane = threadIdx.x & 63u;\n");
+    e("  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
+    const char* const PA = opt.argload ? "ka->" : "a.";
+    if (opt.argload)
+        e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
+          "  const KArgs ka0 = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();\n");
+    auto launder = [&](const char* indent) {
+        if (opt.argload) e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
+    };
+    e("  __shared__ u32x4 red[%u];  // [row][wave][half][lane] partial planes\n", r * 4 * 2 * 64);
+    e("  u32 s = blockIdx.x / a.cps, c = blockIdx.x - s * a.cps;\n");
+    e("  while (s < a.nstripes) {\n");
+    e("    u64 off = (u64)c * %uu;\n", kBsChunk);
+    e("    if (off > a.sz - %uu) off = a.sz - %uu;  // the last chunk ends at sz (overlapping its neighbour)\n",
+      kBsChunk, kBsChunk);
+    e("    const u64 ub = (u64)s * a.iss + off, uo = (u64)s * a.oss + off;\n");
+    for (unsigned i = 0; i < r; ++i)
+        e("    u32 a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7;\n", i, i, i, i, i, i, i, i);
+    const unsigned pf = opt.prefetch ? opt.prefetch : 1;
+    for (unsigned w = 0; w < 4; ++w) {
+        const unsigned j0 = w * k / 4, j1 = (w + 1) * k / 4;
+        e("    if (wave == %uu) {  // inputs %u..%u\n", w, j0, j1 - 1);
+        launder("    ");
+        auto emit_load = [&](unsigned j) {
+            e("    const __amdgpu_buffer_rsrc_t ri%u = rs(%sin[%u] + ub);\n", j, PA, j);
+            e("    const u32x4 l%u_0 = ld(ri%u, lo16), l%u_1 = ld(ri%u, lo16 + 1024u);\n", j, j, j, j);
+        };
+        for (unsigned j = j0; j < j0 + pf && j < j1; ++j) emit_load(j);
+        std::vector<char> init(size_t(r) * 8, 0);
+        for (unsigned j = j0; j < j1; ++j) {
+            if (j + pf < j1) emit_load(j + pf);
+            e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", j, j, j, j, j, j, j, j);
+            e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", j, j, j, j, j, j, j, j);
+            e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", j, j, j, j, j, j, j, j);
+            emit_updates(e, masks, k, j, j, 0, r, init);
+            if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
+        }
+        for (unsigned i = 0; i < r; ++i) {
+            for (unsigned b = 0; b < 8; ++b)
+                if (!init[size_t(i) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
+            e("    red[%uu + lane] = u32x4{a%u_0, a%u_1, a%u_2, a%u_3};\n", (i * 4 + w) * 128, i, i, i, i);
+            e("    red[%uu + lane] = u32x4{a%u_4, a%u_5, a%u_6, a%u_7};\n", (i * 4 + w) * 128 + 64, i, i, i, i);
+        }
+        e("    }\n");
+    }
+    e("    __syncthreads();\n");
+    for (unsigned i = 0; i < r; ++i) {
+        e("    if (wave == %uu) {  // row %u: the 4 partials\n", i % 4, i);
+        launder("    ");
+        e("    const u32x4 p%u_0 = red[%uu + lane] ^ red[%uu + lane] ^ red[%uu + lane] ^ red[%uu + lane];\n", i,
+          (i * 4 + 0) * 128, (i * 4 + 1) * 128, (i * 4 + 2) * 128, (i * 4 + 3) * 128);
+        e("    const u32x4 p%u_1 = red[%uu + lane] ^ red[%uu + lane] ^ red[%uu + lane] ^ red[%uu + lane];\n", i,
+          (i * 4 + 0) * 128 + 64, (i * 4 + 1) * 128 + 64, (i * 4 + 2) * 128 + 64, (i * 4 + 3) * 128 + 64);
+        e("    a%u_0 = p%u_0.x; a%u_1 = p%u_0.y; a%u_2 = p%u_0.z; a%u_3 = p%u_0.w;\n", i, i, i, i, i, i, i, i);
+        e("    a%u_4 = p%u_1.x; a%u_5 = p%u_1.y; a%u_6 = p%u_1.z; a%u_7 = p%u_1.w;\n", i, i, i, i, i, i, i, i);
+        e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
+        e("    const __amdgpu_buffer_rsrc_t ro%u = rs(%sout[%u] + uo);\n", i, PA, i);
+        e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
+        e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
+        e("    }\n");
+    }
+    e("    __syncthreads();  // every wave has read the partials before the next unit's overwrite\n");
+    e("    c += a.gs_c;\n    s += a.gs_s;\n    if (c >= a.cps) { c -= a.cps; ++s; }\n  }\n}\n");
+    return e.s;
+}
+}  // namespace
+
 std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name) {
     field_init();
+    if (bitslice_ksplit(k, r, opt) && opt.probe == 0) {
+        std::vector<uint8_t> masks(size_t(r) * k * 8);
+        for (unsigned i = 0; i < r; ++i)
+            for (unsigned j = 0; j < k; ++j) coef_masks(coef[i * k + j], &masks[(size_t(i) * k + j) * 8]);
+        return source_ksplit(masks, k, r, opt, name);
+    }
     const unsigned ntiles = bitslice_tiles(r, opt);
     std::vector<unsigned> tile_lo(ntiles + 1);
     for (unsigned t = 0; t <= ntiles; ++t) tile_lo[t] = t * r / ntiles;  // near-equal tiles
@@ -631,6 +752,7 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     if (opt.shift64) key += "shift64/";
     if (opt.share && bitslice_split(r, opt)) key += "share/";
     if (opt.probe) key += "probe" + std::to_string(opt.probe) + "/";
+    if (bitslice_ksplit(k, r, opt) && !opt.probe) key += "ksplit/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;
 }
@@ -646,8 +768,9 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     char nm[80];
     snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
     e->name = nm;
+    const bool ks = bitslice_ksplit(k, r, opt) && opt.probe == 0;
     e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
-    e->units_per_block = bitslice_split(r, opt) ? 1 : 4;
+    e->units_per_block = bitslice_split(r, opt) || ks ? 1 : 4;
     R.entries.emplace(key, std::move(ne));
     ++R.pending;
     std::string src = bitslice_source(coef, k, r, opt, nm);

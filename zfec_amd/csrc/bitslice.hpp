@@ -40,6 +40,8 @@ struct BsOptions {
     bool argload = true;             // block pointers loaded where used (no up-front SGPR spill)
     bool shift64 = true;             // bit transposes shift register pairs with 64-bit shifts (4-9 % fewer
                                      // VALU; cfg4 decode 380 -> 375 us, encode unchanged: profiles/r02_jit_shift64.log)
+    bool ksplit = true;              // one row tile and k > 32: a unit's inputs split over the 4 waves of a
+                                     // workgroup, partial planes reduced through LDS (4x the waves per unit)
     unsigned probe = 0;              // measurement variants (tools/jit_probe.py; results NOT the code's):
                                      // 1 = no HBM traffic (inputs synthesised, stores dropped),
                                      // 2 = no arithmetic (same loads and stores, outputs = XOR of raw inputs)
@@ -54,6 +56,9 @@ constexpr unsigned kJitMaxCoef = 1600;
 // workgroup (2-8 tiles) or each wave walks all of them.
 unsigned bitslice_tiles(unsigned r, const BsOptions& opt);
 bool bitslice_split(unsigned r, const BsOptions& opt);
+// Whether the kernel for k inputs and r rows splits its inputs over the waves
+// of a workgroup (BsOptions::ksplit).
+bool bitslice_ksplit(unsigned k, unsigned r, const BsOptions& opt);
 
 // Source of the kernel `name` for the r x k matrix `coef` (row-major).
 std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name);

@@ -53,6 +53,7 @@ Config* read_env() {
     o.share = env_uint("ZFEC_HIP_JIT_SHARE", o.share ? 1 : 0) != 0;
     o.argload = env_uint("ZFEC_HIP_JIT_ARGLOAD", o.argload ? 1 : 0) != 0;
     o.shift64 = env_uint("ZFEC_HIP_JIT_SHIFT64", o.shift64 ? 1 : 0) != 0;
+    o.ksplit = env_uint("ZFEC_HIP_JIT_KSPLIT", o.ksplit ? 1 : 0) != 0;
     c->jit_lds = env_uint("ZFEC_HIP_JIT_LDS", 0);
     if (c->jit_lds > (96u << 10)) c->jit_lds = 96u << 10;
     o.probe = env_uint("ZFEC_HIP_JIT_PROBE", 0);

@@ -306,14 +306,15 @@ int apply_matrix_range(const uint8_t* coef, unsigned coef_stride, unsigned k, un
     const size_t stripes_per_launch = std::max<size_t>(1, config().launch_units / cps);
     // wide codes: every input in one bit-sliced pass per row group
     const bool wide = k > static_cast<unsigned>(kMaxIn) &&
-                      wide_launch_ok(k, std::min<unsigned>(r, kMaxOut), sz, std::min(stripes_per_launch, nstripes));
+                      wide_launch_ok(k, r, sz, std::min(stripes_per_launch, nstripes));
     const unsigned kstep = wide ? k : static_cast<unsigned>(kMaxIn);
     const uint8_t* pin[kMaxWideIn];
     uint8_t* pout[kMaxWideIn];
     for (unsigned j0 = 0; j0 < k; j0 += kstep) {
         const unsigned kg = std::min<unsigned>(kstep, k - j0);
-        const unsigned rmax = wide ? static_cast<unsigned>(kMaxOut)
-                                   : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
+        // wide: every row in one launch (matapply_bsg walks row groups itself,
+        // the JIT takes k * r <= kJitMaxCoef)
+        const unsigned rmax = wide ? r : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / kg));
         const unsigned ngroups = (r + rmax - 1) / rmax;
         for (unsigned g = 0; g < ngroups; ++g) {
             // near-equal row groups

@@ -787,15 +787,17 @@ __host__ __device__ constexpr uint32_t bsg_phase_bytes() {
 
 struct alignas(16) BsgTblJob {
     uint64_t sz, in_sstride, out_sstride;
-    uint32_t nstripes, k, r, cps, gs_c, gs_s, pad0_, pad1_;
-    const uint8_t* table;  // device memory: k input pointers, r output pointers, walk-order coefficients
+    uint32_t nstripes, k, r, cps, gs_c, gs_s;
+    uint32_t ngroups;  // row groups of 4 * RT rows: workgroup units are (group, stripe, unit) triples
+    uint32_t pad_;
+    const uint8_t* table;  // device memory: k input pointers, r output pointers, per group the walk-order coefficients
 };
 
 typedef const __attribute__((address_space(4))) uint64_t* CU64;
 typedef const __attribute__((address_space(4))) uint32_t* KWords;
 
 // Block pointers and coefficient words of a launch: from the kernel arguments
-// (MatJob) or from the device-side table (scalar loads either way).
+// (MatJob, one row group) or from the device-side table (scalar loads either way).
 struct BsgKarg {
     KPtr<MatJob> kj;
     __device__ const uint8_t* in(uint32_t j) const { return kj->in[j]; }
@@ -833,7 +835,14 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
         else
             return BsgKarg{kernarg_job<MatJob>()};
     }();
-    const KWords cw = src.coef() + wave * nph * ND;  // this wave's phases
+    // The walk's "stripes" are (row group, stripe) pairs, group-major (one group
+    // without the table): a launch with few units of work per row group still
+    // fills the chip, each workgroup building the combinations of its unit's
+    // inputs for its group's rows.
+    const uint32_t ns = job.nstripes;
+    uint32_t nvs = ns;
+    if constexpr (TBL) nvs = ns * job.ngroups;
+    const uint32_t rpg = 4u * static_cast<uint32_t>(RT);  // rows per group
     const uint64_t sz = job.sz;
     // byte offset of unit c in a block: the last unit of a block ends at sz
     // (overlapping its neighbour)
@@ -841,34 +850,38 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
         uint64_t o = static_cast<uint64_t>(cu) * kBsgChunk;
         return o > sz - kBsgChunk ? sz - kBsgChunk : o;
     };
+    auto stripe_of = [&](uint32_t vs) { return TBL ? vs % ns : vs; };
     const bool builder = wave < static_cast<uint32_t>(P);
     // the input this wave transposes next, loaded one phase ahead (the next
     // unit's first phase while the current unit's last phase computes), so a
     // phase never starts waiting on HBM
     u32x4 xin[4];
-    auto load_input = [&](uint32_t su, uint32_t cu, uint32_t j) {
-        const uint8_t* ip = src.in(j) + (su * job.in_sstride + unit_off(cu) + lane * 16u);
+    auto load_input = [&](uint32_t vs, uint32_t cu, uint32_t j) {
+        const uint8_t* ip = src.in(j) + (stripe_of(vs) * job.in_sstride + unit_off(cu) + lane * 16u);
         xin[0] = load16(ip);
         xin[1] = load16(ip + 1024);
         xin[2] = load16(ip + 2048);
         xin[3] = load16(ip + 3072);
     };
-    uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
-    if (builder && s < job.nstripes && wave < k) load_input(s, c, wave);
-    while (s < job.nstripes) {
+    uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;  // s: (group, stripe) index
+    if (builder && s < nvs && wave < k) load_input(s, c, wave);
+    while (s < nvs) {
         uint32_t s2 = s + job.gs_s, c2 = c + job.gs_c;  // this workgroup's next unit
         if (c2 >= job.cps) {
             c2 -= job.cps;
             ++s2;
         }
-        const uint64_t ob = s * job.out_sstride + unit_off(c) + lane * 16u;
+        const uint32_t g = TBL ? s / ns : 0u;  // row group
+        const uint32_t row0 = g * rpg, rows = r - row0 < rpg ? r - row0 : rpg;
+        const KWords cw = src.coef() + (g * 4u + wave) * nph * ND;  // this wave's phases
+        const uint64_t ob = stripe_of(s) * job.out_sstride + unit_off(c) + lane * 16u;
         uint32_t acc[RT][2][8];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr)
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
+            for (int gg = 0; gg < 2; ++gg)
 #pragma unroll
-                for (int b = 0; b < 8; ++b) acc[rr][g][b] = 0u;
+                for (int b = 0; b < 8; ++b) acc[rr][gg][b] = 0u;
         for (uint32_t f = 0; f < nph; ++f) {
             const uint32_t j0 = f * P;
             // build: input j0 + wave into slot wave
@@ -887,7 +900,7 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
             if (builder) {  // prefetch: this unit's next phase, else the next unit's first
                 if (f + 1 < nph) {
                     if (jb + P < k) load_input(s, c, jb + P);
-                } else if (s2 < job.nstripes && wave < k) {
+                } else if (s2 < nvs && wave < k) {
                     load_input(s2, c2, wave);
                 }
             }
@@ -928,10 +941,10 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
             const uint32_t i = wave + 4u * rr;
-            if (i >= r) break;  // wave-uniform
+            if (i >= rows) break;  // wave-uniform
             transpose8(acc[rr][0]);
             transpose8(acc[rr][1]);
-            uint8_t* op = src.out(i) + ob;
+            uint8_t* op = src.out(row0 + i) + ob;
             store16_out<true>(op, u32x4{acc[rr][0][0], acc[rr][0][1], acc[rr][0][2], acc[rr][0][3]});
             store16_out<true>(op + 1024, u32x4{acc[rr][0][4], acc[rr][0][5], acc[rr][0][6], acc[rr][0][7]});
             store16_out<true>(op + 2048, u32x4{acc[rr][1][0], acc[rr][1][1], acc[rr][1][2], acc[rr][1][3]});
@@ -1282,8 +1295,11 @@ void fill_bsg() {
 }
 
 bool bsg_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    // k * r >= 24, not a register-kernel shape; past 32 inputs (the table form)
+    // up to 256 rows in one launch, otherwise one group of <= 48
+    const uint32_t rmax = k > static_cast<uint32_t>(kMaxIn) ? 256u : kBsgMaxRows;
     return generic_mode() != 0 && sz >= kBsgChunk && k >= 1 && k <= static_cast<uint32_t>(kMaxWideIn) && r >= 1 &&
-           r <= kBsgMaxRows && k * r >= 24 && !(k <= 4 && r <= 8);
+           r <= rmax && k * r >= 24 && !(k <= 4 && r <= 8);
 }
 
 // Device-side argument tables of wide matapply_bsg launches, per thread and
@@ -1292,7 +1308,7 @@ bool bsg_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
 // last launch has completed.
 struct TableRing {
     static constexpr int kSlots = 8;
-    static constexpr size_t kSlotBytes = size_t(16) << 10;
+    static constexpr size_t kSlotBytes = size_t(160) << 10;  // k, r <= 256 with 64 row groups of 4
     uint8_t* dev = nullptr;
     uint8_t* host = nullptr;
     hipEvent_t ev[kSlots] = {};
@@ -1344,33 +1360,48 @@ hipError_t ring_slot(TableRing** ring, unsigned* slot) {
 hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsg_once, [] { fill_bsg<0>(); });
     const uint32_t k = a.k, r = a.r;
-    const uint32_t need_rt = (r + 3) / 4;
-    int ri = 0;
-    while (kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
-    const BsgVariant& v = g_bsg_var[ri];
-    // coefficients in the kernel's walk order: wave w's bytes of phase f at
-    // (w * nph + f) * PB, (js, rr) in order: row w + 4 * rr of input 2 * f + js
-    const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = kBsgPhase;
-    const uint32_t PB = (P * RT + 3) / 4 * 4, nph = (k + P - 1) / P;
-    const uint32_t walk = 4u * nph * PB;
-    auto fill_walk = [&](uint8_t* cf) {
-        std::memset(cf, 0, walk);
-        for (uint32_t w = 0; w < 4; ++w)
-            for (uint32_t f = 0; f < nph; ++f)
-                for (uint32_t js = 0; js < P; ++js)
-                    for (uint32_t rr = 0; rr < RT; ++rr) {
-                        const uint32_t i = w + 4 * rr, j = P * f + js;
-                        if (i < r && j < k) cf[(w * nph + f) * PB + js * RT + rr] = a.coef[size_t(i) * a.coef_stride + j];
-                    }
-    };
-    const size_t lds = size_t(P) * kBsgSlotBytes;
     const uint64_t cps = (a.sz + kBsgChunk - 1) / kBsgChunk;
     const uint64_t units = cps * a.nstripes;
-    if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
+    // Rows per wave: the smallest instantiated RT >= ceil(r / 4), at most 12
+    // (48 rows per group of the walk).  A launch with fewer than ~4 workgroups
+    // per CU of (unit, row group) work takes smaller row groups: each group's
+    // workgroups rebuild the inputs' combinations, which costs less than idle
+    // CUs (a 64 MiB stripe of a 128/256 code is 128 units of 4 KiB).
+    const uint32_t need_rt = (r + 3) / 4;
+    int ri = 0;
+    while (ri + 1 < kBsgNumRT && kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
+    const uint64_t target = 4ull * static_cast<uint64_t>(g_num_cu);
+    auto groups_of = [&](int i) { return (r + 4u * kBsgRT[i] - 1) / (4u * kBsgRT[i]); };
+    while (ri > 0 && units * groups_of(ri) < target) --ri;
+    const uint32_t ngroups = groups_of(ri);
+    const BsgVariant& v = g_bsg_var[ri];
+    // coefficients in the kernel's walk order: group g, wave w, phase f at
+    // ((g * 4 + w) * nph + f) * PB, (js, rr) in order: row g * 4 * RT + w + 4 * rr
+    // of input 2 * f + js
+    const uint32_t RT = static_cast<uint32_t>(kBsgRT[ri]), P = kBsgPhase;
+    const uint32_t PB = (P * RT + 3) / 4 * 4, nph = (k + P - 1) / P;
+    const uint32_t walk = ngroups * 4u * nph * PB;
+    auto fill_walk = [&](uint8_t* cf) {
+        std::memset(cf, 0, walk);
+        for (uint32_t g = 0; g < ngroups; ++g)
+            for (uint32_t w = 0; w < 4; ++w)
+                for (uint32_t f = 0; f < nph; ++f)
+                    for (uint32_t js = 0; js < P; ++js)
+                        for (uint32_t rr = 0; rr < RT; ++rr) {
+                            const uint32_t i = g * 4 * RT + w + 4 * rr, j = P * f + js;
+                            if (i < r && j < k && w + 4 * rr < 4 * RT)
+                                cf[((g * 4 + w) * nph + f) * PB + js * RT + rr] =
+                                    a.coef[size_t(i) * a.coef_stride + j];
+                        }
+    };
+    const size_t lds = size_t(P) * kBsgSlotBytes;
+    const uint64_t vunits = units * ngroups;
+    if (vunits >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
     const uint64_t cap = uint64_t(g_num_cu) * v.blocks_per_cu * 8;
-    const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    const uint32_t grid = static_cast<uint32_t>(vunits < cap ? vunits : cap);
     const uint32_t gs_s = static_cast<uint32_t>(grid / cps), gs_c = static_cast<uint32_t>(grid % cps);
-    if (k <= static_cast<uint32_t>(kMaxIn) && walk <= static_cast<uint32_t>(kMaxCoef)) {
+    if (ngroups == 1 && k <= static_cast<uint32_t>(kMaxIn) && r <= static_cast<uint32_t>(kMaxOut) &&
+        walk <= static_cast<uint32_t>(kMaxCoef)) {
         MatJob job;
         fill_matjob(a, job);
         fill_walk(job.coef);
@@ -1382,7 +1413,7 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
         t_last_kernel = v.name;
         return hipGetLastError();
     }
-    // wide: pointers and coefficients in a device-side table
+    // pointers and coefficients in a device-side table
     const size_t bytes = 8 * size_t(k + r) + walk;
     if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
     TableRing* ring = nullptr;
@@ -1405,7 +1436,8 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = gs_s;
     job.gs_c = gs_c;
-    job.pad0_ = job.pad1_ = 0;
+    job.ngroups = ngroups;
+    job.pad_ = 0;
     job.table = d;
     hipLaunchKernelGGL(reinterpret_cast<void (*)(const BsgTblJob)>(const_cast<void*>(v.fn_tbl)), dim3(grid),
                        dim3(256), lds, stream, job);
@@ -1462,10 +1494,10 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     t_signal_used = false;
     std::call_once(g_dispatch_once, init_dispatch);
     const uint32_t k = a.k, r = a.r;
-    if (k == 0 || r == 0 || a.nstripes == 0 || a.sz == 0 || a.nstripes >= (1ull << 32) || a.coef_stride < k ||
-        k > static_cast<uint32_t>(kMaxWideIn) || r > static_cast<uint32_t>(kMaxOut))
-        return hipErrorInvalidValue;
     const bool wide = k > static_cast<uint32_t>(kMaxIn);
+    if (k == 0 || r == 0 || a.nstripes == 0 || a.sz == 0 || a.nstripes >= (1ull << 32) || a.coef_stride < k ||
+        k > static_cast<uint32_t>(kMaxWideIn) || r > (wide ? 256u : static_cast<uint32_t>(kMaxOut)))
+        return hipErrorInvalidValue;
     if (!wide && k * r > static_cast<uint32_t>(kMaxCoef)) return hipErrorInvalidValue;
     if (!a.accumulate) {  // a run-time specialised bit-sliced kernel, where one applies and is compiled
         const char* jit_name = nullptr;
