@@ -14,26 +14,29 @@ EXT      := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('E
 SRC      := zfec_amd/csrc
 LIB      := zfec_amd/libzfec_hip.so
 PYEXT    := zfec_amd/_fec$(EXT)
+# every object depends on every header: config.hpp embeds bitslice.hpp's options, so a
+# header change must rebuild all of them (a stale object reads a stale Config layout)
+HDRS     := $(wildcard $(SRC)/*.hpp) include/zfec_hip.h
 HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function
 
 all: $(LIB) $(PYEXT) oracle
 
-$(SRC)/kernels.o: $(SRC)/kernels.hip $(SRC)/kernels.hpp $(SRC)/bitslice.hpp $(SRC)/config.hpp
+$(SRC)/kernels.o: $(SRC)/kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/config.hpp
+$(SRC)/bitslice.o: $(SRC)/bitslice.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(SRC)/kernels.hpp $(SRC)/gf256.hpp $(SRC)/host_pool.hpp $(SRC)/config.hpp include/zfec_hip.h
+$(SRC)/fec_abi.o: $(SRC)/fec_abi.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/gf256.o: $(SRC)/gf256.cpp $(SRC)/gf256.hpp
+$(SRC)/gf256.o: $(SRC)/gf256.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(SRC)/host_pool.o: $(SRC)/host_pool.cpp $(SRC)/host_pool.hpp
+$(SRC)/host_pool.o: $(SRC)/host_pool.cpp $(HDRS)
 	$(CXX) -O2 -std=c++17 -fPIC -fvisibility=hidden -Wall -c $< -o $@
 
-$(SRC)/config.o: $(SRC)/config.cpp $(SRC)/config.hpp $(SRC)/bitslice.hpp $(SRC)/kernels.hpp
+$(SRC)/config.o: $(SRC)/config.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(SRC)/kernels.o $(SRC)/fec_abi.o $(SRC)/gf256.o $(SRC)/bitslice.o $(SRC)/host_pool.o $(SRC)/config.o

@@ -908,6 +908,28 @@ int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& 
         if (index[i] < k && index[i] != i)
             return set_status(FEC_EINVAL, "primary block %u must be at slot %u, found at slot %u", index[i], index[i], i);
     }
+    // The inverse is O(k^3) on the host (255 x 255 with 128 secondaries:
+    // ~0.8 ms, more than the kernel), and batches of stripes are decoded from
+    // the same blocks call after call, so each thread keeps its last few
+    // decode matrices.  The key is (k, index): the encoding matrix's row b
+    // depends on k and b only, not on n (zfec/fec.c:456-469; checked against
+    // the reference).
+    struct Cached {
+        unsigned k = 0;
+        bool all = false;
+        std::vector<unsigned> idx;
+        std::vector<uint8_t> rows;
+        unsigned r = 0;
+    };
+    constexpr int kCache = 8;
+    thread_local Cached cache[kCache];
+    thread_local unsigned next = 0;
+    for (const Cached& c : cache)
+        if (c.k == k && c.all == all_primaries && std::equal(index, index + k, c.idx.begin(), c.idx.end())) {
+            rows.assign(c.rows.begin(), c.rows.end());
+            r = c.r;
+            return FEC_OK;
+        }
     thread_local std::vector<uint8_t> dec;
     dec.resize(size_t(k) * k);
     if (!build_decode_matrix(code->enc_matrix, k, index, dec.data()))
@@ -919,6 +941,12 @@ int decode_rows(const fec_t* code, const unsigned* index, std::vector<uint8_t>& 
         rows.insert(rows.end(), dec.begin() + size_t(i) * k, dec.begin() + size_t(i + 1) * k);
         ++r;
     }
+    Cached& c = cache[next++ % kCache];
+    c.k = k;
+    c.all = all_primaries;
+    c.idx.assign(index, index + k);
+    c.rows.assign(rows.begin(), rows.end());
+    c.r = r;
     return FEC_OK;
 }
 
