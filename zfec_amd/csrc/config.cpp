@@ -38,6 +38,7 @@ Config* read_env() {
     const char* s = env("ZFEC_HIP_STORE");
     c->store = s && !strcmp(s, "nt") ? kStoreNt : s && !strcmp(s, "ntsc1") ? kStoreNtSc1 : kStoreAuto;
     c->small_lanes = env_size("ZFEC_HIP_SMALL_LANES", 2048);
+    c->bsg_wgs_per_cu = env_uint("ZFEC_HIP_BSG_WGS", 4);
 
     BsOptions& o = c->jit;
     o.max_tile = env_uint("ZFEC_HIP_JIT_TILE", o.max_tile);

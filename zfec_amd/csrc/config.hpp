@@ -23,6 +23,7 @@ struct Config {
     bool batch_collapse;   // ZFEC_HIP_BATCH_COLLAPSE=0: block-major batches are not collapsed into one stripe
     StorePolicy store;     // ZFEC_HIP_STORE=auto|nt|ntsc1: output store policy of the register kernels
     uint64_t small_lanes;  // ZFEC_HIP_SMALL_LANES: launches below this many lanes take matapply_small (0: never)
+    unsigned bsg_wgs_per_cu;  // ZFEC_HIP_BSG_WGS: matapply_bsg takes smaller row groups below this many workgroups per CU
     BsOptions jit;         // ZFEC_HIP_JIT_*: code-generation options of the bit-sliced JIT kernels
     unsigned jit_lds;      // ZFEC_HIP_JIT_LDS: extra dynamic LDS bytes per JIT workgroup (A/B: caps residency)
     // host paths

@@ -1370,7 +1370,7 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     const uint32_t need_rt = (r + 3) / 4;
     int ri = 0;
     while (ri + 1 < kBsgNumRT && kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
-    const uint64_t target = 4ull * static_cast<uint64_t>(g_num_cu);
+    const uint64_t target = uint64_t(config().bsg_wgs_per_cu) * static_cast<uint64_t>(g_num_cu);
     auto groups_of = [&](int i) { return (r + 4u * kBsgRT[i] - 1) / (4u * kBsgRT[i]); };
     while (ri > 0 && units * groups_of(ri) < target) --ri;
     const uint32_t ngroups = groups_of(ri);
