@@ -219,7 +219,7 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-PROFILE_ROUND = "r02"
+PROFILE_ROUND = "r03"
 
 
 def pmc_traffic(workload, leg="encode cold"):

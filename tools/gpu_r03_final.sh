@@ -12,4 +12,5 @@ for W in cfg3 cfg4 cfg5; do
 done
 bash tools/profile_r02.sh ${T}prof cfg2 cfg3 cfg4 cfg5 > gpurun_out/${T}_profile.log 2>&1
 timeout -k 10 300 python tools/bytes_latency.py > gpurun_out/${T}_bytes_latency.log 2>&1
+timeout -k 10 300 python tools/wide_bench.py --variants shipped > gpurun_out/${T}_wide.json 2> gpurun_out/${T}_wide.log
 echo done

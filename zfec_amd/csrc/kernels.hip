@@ -1366,13 +1366,17 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     // (48 rows per group of the walk).  A launch with fewer than ~4 workgroups
     // per CU of (unit, row group) work takes smaller row groups: each group's
     // workgroups rebuild the inputs' combinations, which costs less than idle
-    // CUs (a 64 MiB stripe of a 128/256 code is 128 units of 4 KiB).
+    // CUs (a 64 MiB stripe of a 128/256 code is 128 units of 4 KiB).  The
+    // shrinking stops at RT 2: one row per wave re-reads every input per 4
+    // rows, and measured slower than half-idle CUs (profiles/r03_bsg_wgs.json:
+    // 200/256 at RT 2 0.207 ms, RT 1 0.278 ms; 128/256 at RT 4 0.249 ms, RT 10
+    // 0.351 ms, RT 2 0.312 ms).
     const uint32_t need_rt = (r + 3) / 4;
     int ri = 0;
     while (ri + 1 < kBsgNumRT && kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
     const uint64_t target = uint64_t(config().bsg_wgs_per_cu) * static_cast<uint64_t>(g_num_cu);
     auto groups_of = [&](int i) { return (r + 4u * kBsgRT[i] - 1) / (4u * kBsgRT[i]); };
-    while (ri > 0 && units * groups_of(ri) < target) --ri;
+    while (ri > 1 && units * groups_of(ri) < target) --ri;
     const uint32_t ngroups = groups_of(ri);
     const BsgVariant& v = g_bsg_var[ri];
     // coefficients in the kernel's walk order: group g, wave w, phase f at
