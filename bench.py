@@ -102,6 +102,9 @@ def parse():
                         "stream, joined once after the timed steps, so short launches overlap each other's "
                         "ramp-up and drain (default: 2 for the K=3/M=10 workloads cfg2/cfg5, 1 for the bit-sliced "
                         "wide codes cfg3/cfg4, where co-resident launches measured slower; DESIGN.md section 5)")
+    p.add_argument("--paired", action="store_true",
+                   help="each step as ONE fec_run_batch_jobs call on one stream: its encode and decode share one "
+                        "matapply_pair launch where both are register-kernel shapes (cfg2), else one launch each")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
@@ -491,7 +494,7 @@ def back_to_back(fns, n, stream, leg):
 
 
 def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256", row_padding=True, fresh=0,
-                 streams=1):
+                 streams=1, paired=False):
     """Encode + decode `ns` stripes per step; returns timings.
 
     HBM layout: [stripe][block][row_stride] with the row stride = sz rounded up
@@ -585,7 +588,25 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
 
         launch = "eager, 2 streams (encodes | decodes)"
 
-    if use_graph and streams == 1:
+    if paired:
+        # one fec_run_batch_jobs call per step: the two independent jobs share
+        # one launch (matapply_pair) where both are register-kernel shapes
+        jobs = capi.BatchJobs([
+            capi.encode_job(code, data[0].data_ptr(), ld, k * ld, par[0].data_ptr(), ld, r * ld, enc_nums, sz, ns,
+                            flags=fl & capi.FEC_FLAG_ROW_PADDING),
+            capi.decode_job(code, recv[0].data_ptr(), ld, k * ld, rec[0].data_ptr(), ld, nrec * ld, slots, sz, ns,
+                            flags=fl & capi.FEC_FLAG_ROW_PADDING)])
+        jobs.run(stream.cuda_stream)
+        kernels["step"] = capi.last_kernel_name()
+        torch.cuda.synchronize()
+
+        def step():
+            jobs.run(stream.cuda_stream)
+
+        fork = join = lambda: None
+        launch = "one fec_run_batch_jobs call per step (%s)" % kernels["step"]
+
+    if use_graph and streams == 1 and not paired:
         try:
             cap = torch.cuda.Stream()
             graph = torch.cuda.CUDAGraph()
@@ -608,6 +629,8 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
         if launch.startswith("eager"):
             LEGS.add("warmup", kernels["encode"])
             LEGS.add("warmup", kernels["decode"])
+        elif paired:
+            LEGS.add("warmup", kernels["step"])
     join()
     torch.cuda.synchronize()
     nbar = NodeBarrier(dist, dist.get_rank() if dist else 0, dist.get_world_size() if dist else 1)
@@ -633,6 +656,9 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
         for _ in range(steps):
             LEGS.add("timed loop", kernels["encode"])
             LEGS.add("timed loop", kernels["decode"])
+    elif paired:
+        for _ in range(steps):
+            LEGS.add("timed loop", kernels["step"])
 
     # Per-kernel launch duration for the rooflines: back-to-back launches of
     # one kernel between two HIP events on the launch stream, (a) "warm": the
@@ -789,9 +815,9 @@ def main():
         ns = nstripes
     fresh = args.fresh if args.fresh is not None else (20 if args.workload in ("cfg3", "cfg4") else 0)
     if args.streams is None:
-        args.streams = 1 if args.workload in ("cfg3", "cfg4") else 2
+        args.streams = 1 if args.workload in ("cfg3", "cfg4") or args.paired else 2
     t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout,
-                     streams=args.streams,
+                     streams=args.streams, paired=args.paired,
                      row_padding=not args.no_row_padding, fresh=fresh if rank == 0 else 0)
     el = reduce(dist, t["elapsed_s"], dist.ReduceOp.MAX if dist else None)
     total_bytes = reduce(dist, float(args.steps * 2 * k * sz * ns), dist.ReduceOp.SUM if dist else None)
@@ -864,7 +890,7 @@ def main():
                             "rw_ceiling": rw_ceiling(k * sz * ns, nrec * sz * ns, gbps(dec_bytes, t["dec_ms"]))},
         "valu_roofline": None if args.slabs else valu_roofline(args.workload, t["kernels"]["encode"], t["enc_ms"]),
         "launch": t["launch"],
-        "streams": args.streams,
+        "streams": args.streams, "paired": args.paired,
         "gpu_ms_per_step": round(t["gpu_step_ms"], 4),
         "encode_input_GBps": round(gbps(k * sz * ns, t["enc_ms"]), 1),
         "decode_input_GBps": round(gbps(k * sz * ns, t["dec_ms"]), 1),

@@ -174,6 +174,41 @@ int fec_decode_batch_multi(const fec_t* code,
                            const unsigned* index, size_t sz, size_t nstripes,
                            const int* devices, size_t ndevices, unsigned flags);
 
+/* Several batched calls in one: job i is exactly the fec_encode_batch
+ * (kind FEC_JOB_ENCODE: nums = block_nums, num_nums entries) or
+ * fec_decode_batch (kind FEC_JOB_DECODE: nums = index, k entries; num_nums
+ * ignored) call its fields describe, with its own flags (only
+ * FEC_FLAG_ROW_PADDING and FEC_FLAG_ALL_PRIMARIES apply per job).  The jobs
+ * are independent: they may run concurrently and in any order, so no job may
+ * read or write a buffer another job writes.  Two consecutive jobs on one
+ * device, over codes with the same k and of register-kernel shape (k <= 4,
+ * at most 8 outputs each, the narrower job at most k outputs; blocks longer
+ * than 4 KiB or fewer than 64 stripes) share ONE launch, which pays one launch
+ * ramp-up and drain instead of two (a stripe's encode next to another
+ * stripe's decode); other jobs launch one at a time on the same stream.
+ * `stream` and `flags` (FEC_FLAG_ASYNC, FEC_FLAG_LIBRARY_STREAM) apply to the
+ * whole call.  The first failing job's status is returned, its message
+ * prefixed "job i".  (An extension: zfec/fec.h has no batched calls.)  On the
+ * cfg2 step (a 64 MiB K=3/M=10 stripe's encode and another's decode) one
+ * paired launch per step measured 2465-2514 GB/s against 2506-2529 for the
+ * two launches on two streams and about 2350 on one stream
+ * (profiles/r03_pair_ab.json). */
+#define FEC_JOB_ENCODE 0u
+#define FEC_JOB_DECODE 1u
+typedef struct fec_batch_job {
+    const fec_t* code;
+    unsigned kind;
+    unsigned flags;
+    const gf* src;
+    size_t src_block_stride, src_stripe_stride;
+    gf* dst;
+    size_t dst_block_stride, dst_stripe_stride;
+    const unsigned* nums;
+    size_t num_nums;
+    size_t sz, nstripes;
+} fec_batch_job;
+int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* stream, unsigned flags);
+
 /* Page-locked host memory (hipHostMalloc): host buffers passed to fec_encode /
  * fec_decode from here are read and written by the kernel in place (no
  * per-call pinning, no staging copies).  NULL on failure (status set). */

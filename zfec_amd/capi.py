@@ -56,9 +56,11 @@ SYMBOLS = [
     ("fec_decode_batch_multi", ctypes.c_int, [_P, _P, _SZ, _SZ, _P, _SZ, _SZ, _UP, _SZ, _SZ, _IP, _SZ, _U]),
     ("fec_reload_config", ctypes.c_int, []),
     ("fec_last_wait", ctypes.c_int, []),
+    ("fec_run_batch_jobs", ctypes.c_int, [_P, _SZ, _P, _U]),
 ]
 
 JIT_OFF, JIT_AUTO, JIT_FORCE = 0, 1, 2
+FEC_JOB_ENCODE, FEC_JOB_DECODE = 0, 1
 
 
 class FecT(ctypes.Structure):
@@ -215,3 +217,46 @@ class Code(object):
     def decode_ptrs(self, in_addrs, out_addrs, index, sz, stream=0, flags=FEC_FLAG_ASYNC):
         check(lib().fec_decode_ex(self.ptr, ptr_array(in_addrs), ptr_array(out_addrs), uint_array(index),
                                   sz, stream or None, flags))
+
+
+class BatchJob(ctypes.Structure):
+    """fec_batch_job (include/zfec_hip.h)."""
+
+    _fields_ = [("code", _P), ("kind", _U), ("flags", _U), ("src", _P), ("src_block_stride", _SZ),
+                ("src_stripe_stride", _SZ), ("dst", _P), ("dst_block_stride", _SZ), ("dst_stripe_stride", _SZ),
+                ("nums", _UP), ("num_nums", _SZ), ("sz", _SZ), ("nstripes", _SZ)]
+
+
+def encode_job(code, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, flags=0):
+    """One fec_run_batch_jobs job: Code.encode_batch's arguments."""
+    return (code, FEC_JOB_ENCODE, flags, src, sbs, sss, dst, dbs, dss, tuple(block_nums), sz, nstripes)
+
+
+def decode_job(code, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, flags=0):
+    """One fec_run_batch_jobs job: Code.decode_batch's arguments."""
+    return (code, FEC_JOB_DECODE, flags, src, sbs, sss, dst, dbs, dss, tuple(index), sz, nstripes)
+
+
+class BatchJobs(object):
+    """A fec_run_batch_jobs call built once (the ctypes job array and block
+    number arrays) and run any number of times."""
+
+    def __init__(self, jobs):
+        lib()
+        self._codes = [j[0] for j in jobs]  # keep the fec_t objects alive
+        self._nums = [uint_array(j[9]) for j in jobs]
+        self.n = len(jobs)
+        self._arr = (BatchJob * max(1, self.n))()
+        for i, (code, kind, flags, src, sbs, sss, dst, dbs, dss, nums, sz, ns) in enumerate(jobs):
+            self._arr[i] = BatchJob(code.ptr, kind, flags, src, sbs, sss, dst, dbs, dss,
+                                    ctypes.cast(self._nums[i], _UP), len(nums), sz, ns)
+
+    def run(self, stream=0, flags=FEC_FLAG_ASYNC):
+        st = _lib.fec_run_batch_jobs(self._arr, self.n, stream or None, flags)
+        if st:
+            check(st)
+
+
+def run_batch_jobs(jobs, stream=0, flags=FEC_FLAG_ASYNC):
+    """fec_run_batch_jobs over encode_job / decode_job tuples."""
+    BatchJobs(jobs).run(stream, flags)

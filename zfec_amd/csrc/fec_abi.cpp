@@ -1192,33 +1192,10 @@ FEC_API int fec_jit_prepare_decode(const fec_t* code, const unsigned* index, uns
 }
 
 namespace {
-int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src, size_t sbs, size_t sss, gf* dst,
-              size_t dbs, size_t dss, size_t sz, size_t nstripes, void* stream, unsigned flags) {
-    const unsigned k = code->k;
-    if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
-    if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
-    // one pointer query per side: device memory (its device), or host memory
-    const int sdev = pointer_device(src), ddev0 = pointer_device(dst);
-    // pageable host memory on either side: staged through pinned slots
-    // (synchronous whatever the flags; FEC_FLAG_ROW_PADDING does not apply)
-    if (sz && nstripes && r && (sdev < 0 || ddev0 < 0)) {
-        const size_t src_ext = (nstripes - 1) * sss + (k - 1) * sbs + sz;
-        const size_t dst_ext = (nstripes - 1) * dss + (r - 1) * dbs + sz;
-        const uint8_t* zs = sdev >= 0 ? src : mapped_block(src, src_ext);
-        const uint8_t* zd = ddev0 >= 0 ? dst : mapped_block(dst, dst_ext);
-        if (!zs || !zd) {
-            if (sdev >= 0 && ddev0 >= 0 && sdev != ddev0)
-                return set_status(FEC_EINVAL, "batched entry points take memory on one device");
-            int dev = sdev >= 0 ? sdev : ddev0;
-            if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return set_status(FEC_ENODEV, "no current HIP device");
-            DeviceGuard guard(dev);
-            DevCtx* d = nullptr;
-            if (dev_ctx(dev, &d)) return t_status;
-            hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
-            return run_batch_staged(*d, coef, k, r, zs ? zs : src, sbs, sss, !zs, zd ? const_cast<gf*>(zd) : dst, dbs,
-                                    dss, !zd, sz, nstripes, st);
-        }
-    }
+// The launch geometry of a batched call on device (or page-locked) memory:
+// updates sz and nstripes in place.
+void batch_geometry(unsigned k, unsigned r, size_t sbs, size_t sss, size_t dbs, size_t dss, unsigned flags, size_t& sz,
+                    size_t& nstripes) {
     // Block-major batches (stripes packed back to back inside each block array,
     // both strides == sz) are one stripe of nstripes * sz bytes: output byte x
     // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so
@@ -1247,6 +1224,36 @@ int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src,
     } else {
         sz = grant;
     }
+}
+
+int run_batch(const fec_t* code, const uint8_t* coef, unsigned r, const gf* src, size_t sbs, size_t sss, gf* dst,
+              size_t dbs, size_t dss, size_t sz, size_t nstripes, void* stream, unsigned flags) {
+    const unsigned k = code->k;
+    if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
+    if (!src || !dst) return set_status(FEC_EINVAL, "NULL buffer");
+    // one pointer query per side: device memory (its device), or host memory
+    const int sdev = pointer_device(src), ddev0 = pointer_device(dst);
+    // pageable host memory on either side: staged through pinned slots
+    // (synchronous whatever the flags; FEC_FLAG_ROW_PADDING does not apply)
+    if (sz && nstripes && r && (sdev < 0 || ddev0 < 0)) {
+        const size_t src_ext = (nstripes - 1) * sss + (k - 1) * sbs + sz;
+        const size_t dst_ext = (nstripes - 1) * dss + (r - 1) * dbs + sz;
+        const uint8_t* zs = sdev >= 0 ? src : mapped_block(src, src_ext);
+        const uint8_t* zd = ddev0 >= 0 ? dst : mapped_block(dst, dst_ext);
+        if (!zs || !zd) {
+            if (sdev >= 0 && ddev0 >= 0 && sdev != ddev0)
+                return set_status(FEC_EINVAL, "batched entry points take memory on one device");
+            int dev = sdev >= 0 ? sdev : ddev0;
+            if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return set_status(FEC_ENODEV, "no current HIP device");
+            DeviceGuard guard(dev);
+            DevCtx* d = nullptr;
+            if (dev_ctx(dev, &d)) return t_status;
+            hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
+            return run_batch_staged(*d, coef, k, r, zs ? zs : src, sbs, sss, !zs, zd ? const_cast<gf*>(zd) : dst, dbs,
+                                    dss, !zd, sz, nstripes, st);
+        }
+    }
+    batch_geometry(k, r, sbs, sss, dbs, dss, flags, sz, nstripes);
     // device memory on one device, or page-locked host memory (zero-copy)
     const size_t src_extent = (nstripes - 1) * sss + (k - 1) * sbs + sz;
     const size_t dst_extent = (nstripes - 1) * dss + (r - 1) * dbs + sz;
@@ -1307,6 +1314,157 @@ FEC_API int fec_decode_batch(const fec_t* code, const gf* src, size_t src_block_
     return guarded([&] {
         return run_batch(code, rows.data(), r, src, src_block_stride, src_stripe_stride, dst, dst_block_stride,
                          dst_stripe_stride, sz, nstripes, stream, flags);
+    });
+}
+
+namespace zfec_hip {
+namespace {
+// A fec_run_batch_jobs job resolved for a paired launch (register-kernel
+// shapes: k <= 4, r <= 8).
+struct PairJobSpec {
+    uint8_t coef[4 * 8];
+    unsigned k = 0, r = 0;
+    const uint8_t* in[4];
+    uint8_t* out[8];
+    size_t sz = 0, nstripes = 0, sss = 0, dss = 0;
+    int dev = -1;
+};
+
+// Resolve job j; *ok = false when it cannot share a launch (host memory,
+// another shape, an empty job, more units than one launch takes).
+int resolve_pair_job(const fec_batch_job& j, PairJobSpec& p, bool* ok) {
+    *ok = false;
+    const unsigned k = j.code->k;
+    if (k > 4 || !j.sz || !j.nstripes || !j.src || !j.dst) return FEC_OK;
+    if (j.kind == FEC_JOB_ENCODE) {
+        if (j.num_nums == 0 || j.num_nums > 8) return FEC_OK;
+        p.r = static_cast<unsigned>(j.num_nums);
+        std::memcpy(p.coef, encode_rows(j.code, j.nums, j.num_nums), size_t(p.r) * k);
+    } else {
+        thread_local std::vector<uint8_t> rows;
+        unsigned r = 0;
+        if (decode_rows(j.code, j.nums, rows, r, (j.flags & FEC_FLAG_ALL_PRIMARIES) != 0)) return t_status;
+        if (r == 0 || r > 8) return FEC_OK;
+        p.r = r;
+        std::memcpy(p.coef, rows.data(), size_t(r) * k);
+    }
+    p.k = k;
+    const int sdev = pointer_device(j.src), ddev = pointer_device(j.dst);
+    if (sdev < 0 || sdev != ddev) return FEC_OK;
+    p.dev = sdev;
+    p.sz = j.sz;
+    p.nstripes = j.nstripes;
+    p.sss = j.src_stripe_stride;
+    p.dss = j.dst_stripe_stride;
+    batch_geometry(k, p.r, j.src_block_stride, p.sss, j.dst_block_stride, p.dss, j.flags, p.sz, p.nstripes);
+    // apply_matrix's one-launch condition
+    const size_t cps = (p.sz + kMinChunk - 1) / kMinChunk, max_units = config().launch_units;
+    if (cps > max_units || std::max<size_t>(1, max_units / cps) < p.nstripes) return FEC_OK;
+    for (unsigned i = 0; i < k; ++i) p.in[i] = j.src + i * j.src_block_stride;
+    for (unsigned i = 0; i < p.r; ++i) p.out[i] = j.dst + i * j.dst_block_stride;
+    *ok = true;
+    return FEC_OK;
+}
+
+ApplySpec pair_spec(const PairJobSpec& p) {
+    ApplySpec a;
+    a.coef = p.coef;
+    a.coef_stride = p.k;
+    a.k = p.k;
+    a.r = p.r;
+    a.in = p.in;
+    a.out = p.out;
+    a.sz = p.sz;
+    a.nstripes = p.nstripes;
+    a.in_sstride = p.sss;
+    a.out_sstride = p.dss;
+    a.accumulate = false;
+    return a;
+}
+
+int job_failed(size_t i) {
+    char msg[sizeof t_msg];
+    snprintf(msg, sizeof msg, "%s", t_msg);
+    return set_status(t_status, "job %zu: %s", i, msg);
+}
+}  // namespace
+}  // namespace zfec_hip
+
+FEC_API int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* stream, unsigned flags) {
+    if (njobs && !jobs) return set_status(FEC_EINVAL, "jobs is NULL");
+    for (size_t i = 0; i < njobs; ++i) {
+        const fec_batch_job& j = jobs[i];
+        if (!valid_code(j.code)) return set_status(FEC_EINVAL, "job %zu: invalid fec_t", i);
+        if (j.kind != FEC_JOB_ENCODE && j.kind != FEC_JOB_DECODE)
+            return set_status(FEC_EINVAL, "job %zu: kind %u is neither FEC_JOB_ENCODE nor FEC_JOB_DECODE", i, j.kind);
+        if (j.kind == FEC_JOB_ENCODE && check_block_nums(j.code, j.nums, j.num_nums)) return job_failed(i);
+    }
+    if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
+    return guarded([&] {
+        const unsigned call = flags & (FEC_FLAG_ASYNC | FEC_FLAG_LIBRARY_STREAM);
+        int devs[8];
+        size_t ndevs = 0;
+        auto note_dev = [&](int dev) {
+            for (size_t q = 0; q < ndevs; ++q)
+                if (devs[q] == dev) return;
+            if (ndevs < 8) devs[ndevs++] = dev;
+        };
+        size_t i = 0;
+        while (i < njobs) {
+            if (i + 1 < njobs) {
+                PairJobSpec a, b;
+                bool oka = false, okb = false;
+                if (resolve_pair_job(jobs[i], a, &oka)) return job_failed(i);
+                if (oka && resolve_pair_job(jobs[i + 1], b, &okb)) return job_failed(i + 1);
+                if (oka && okb && a.dev == b.dev && a.k == b.k) {
+                    DeviceGuard guard(a.dev);
+                    DevCtx* d = nullptr;
+                    if (dev_ctx(a.dev, &d)) return t_status;
+                    hipStream_t st = (flags & FEC_FLAG_LIBRARY_STREAM) ? d->stream : static_cast<hipStream_t>(stream);
+                    const hipError_t e = launch_apply_pair(pair_spec(a), pair_spec(b), st);
+                    if (e == hipSuccess) {
+                        ++t_launches;
+                        note_dev(a.dev);
+                        i += 2;
+                        continue;
+                    }
+                    if (e != hipErrorNotSupported) {
+                        hip_fail(e, "launch_apply_pair");
+                        return job_failed(i);
+                    }
+                }
+            }
+            const fec_batch_job& j = jobs[i];
+            const unsigned jf = (j.flags & (FEC_FLAG_ROW_PADDING | FEC_FLAG_ALL_PRIMARIES)) | call | FEC_FLAG_ASYNC;
+            const int st = j.kind == FEC_JOB_ENCODE
+                               ? fec_encode_batch(j.code, j.src, j.src_block_stride, j.src_stripe_stride, j.dst,
+                                                  j.dst_block_stride, j.dst_stripe_stride, j.nums, j.num_nums, j.sz,
+                                                  j.nstripes, stream, jf)
+                               : fec_decode_batch(j.code, j.src, j.src_block_stride, j.src_stripe_stride, j.dst,
+                                                  j.dst_block_stride, j.dst_stripe_stride, j.nums, j.sz, j.nstripes,
+                                                  stream, jf);
+            if (st) return job_failed(i);
+            int dev = pointer_device(j.src);
+            if (dev < 0) dev = pointer_device(j.dst);
+            if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+            note_dev(dev);
+            ++i;
+        }
+        if (!(flags & FEC_FLAG_ASYNC)) {
+            if (!(flags & FEC_FLAG_LIBRARY_STREAM)) {
+                const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+                if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            } else {
+                for (size_t q = 0; q < ndevs; ++q) {
+                    DeviceGuard guard(devs[q]);
+                    DevCtx* d = nullptr;
+                    if (dev_ctx(devs[q], &d)) return t_status;
+                    const hipError_t e = hipStreamSynchronize(d->stream);
+                    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+                }
+            }
+        }
+        return set_status(FEC_OK);
     });
 }
 

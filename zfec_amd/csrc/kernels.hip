@@ -193,8 +193,12 @@ __device__ inline void store_tail(uint8_t* p, u32x4 v, uint32_t nb) {
 struct UnitIter {
     uint32_t s, c;
     template <class J>
-    __device__ explicit UnitIter(const J& job) {
-        const uint32_t gid = blockIdx.x * kBlock + threadIdx.x;
+    __device__ explicit UnitIter(const J& job) : UnitIter(job, blockIdx.x) {}
+    // `block`: the workgroup's index among the job's own workgroups (a paired
+    // launch deals its grid across two jobs)
+    template <class J>
+    __device__ UnitIter(const J& job, uint32_t block) {
+        const uint32_t gid = block * kBlock + threadIdx.x;
         s = gid / job.cps;
         c = gid - s * job.cps;
     }
@@ -237,9 +241,12 @@ __device__ __forceinline__ Span chunk_span(uint32_t c, uint64_t sz, uint32_t nfu
 template <class J>
 using KPtr = const __attribute__((address_space(4))) J*;
 
-template <class J>
+// OFF: the block's byte offset in the argument segment (the second job of a
+// paired launch).
+template <class J, size_t OFF = 0>
 __device__ __forceinline__ KPtr<J> kernarg_job() {
-    KPtr<J> kj = (KPtr<J>)__builtin_amdgcn_kernarg_segment_ptr();
+    typedef const __attribute__((address_space(4))) char* KBytes;
+    KPtr<J> kj = (KPtr<J>)((KBytes)__builtin_amdgcn_kernarg_segment_ptr() + OFF);
     asm volatile("" : "+s"(kj));
     return kj;
 }
@@ -268,7 +275,7 @@ __device__ __forceinline__ Tab reg_table(const RegJob<K, R>& job, uint32_t i) {
 
 // One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.  AL: each
 // row's tables and output pointer are loaded (scalar loads) right before use.
-template <int K, int R, int SP, bool AL>
+template <int K, int R, int SP, bool AL, size_t OFF = 0>
 __device__ __forceinline__ void reg_compute_store(const RegJob<K, R>& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
                                                   uint64_t ob, bool full, uint32_t nb) {
     Sel sel[4][K];
@@ -284,7 +291,7 @@ __device__ __forceinline__ void reg_compute_store(const RegJob<K, R>& job, const
         Tab t[K];
         uint8_t* out;
         if constexpr (AL) {
-            const KPtr<RegJob<K, R>> kj = kernarg_job<RegJob<K, R>>();
+            const KPtr<RegJob<K, R>> kj = kernarg_job<RegJob<K, R>, OFF>();
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t i = (r * K + j) * 5;
@@ -322,8 +329,8 @@ __device__ __forceinline__ void reg_load(const RegJob<K, R>& job, u32x4 (&x)[K],
 // caches the 3-row decode is slower with it, profiles/r02_reg_pf_ab.log).
 // SP: output store policy (store16_pol).  AL: tables and output pointers read
 // where they are used (reg_compute_store).
-template <int K, int R, int SP, bool PF, bool AL>
-__global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
+template <int K, int R, int SP, bool PF, bool AL, size_t OFF>
+__device__ __forceinline__ void reg_body(const RegJob<K, R>& job, uint32_t block) {
     Tab T[R][K];
     if constexpr (!AL) {
 #pragma unroll
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
 
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
-    UnitIter u(job);
+    UnitIter u(job, block);
     if constexpr (PF) {
         u32x4 x[K];
         Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
@@ -346,7 +353,7 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
             const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
             u32x4 xn[K];
             if (v.s < job.nstripes) reg_load<K, R>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
-            reg_compute_store<K, R, SP, AL>(job, T, x, ob, sp.full, sp.nb);
+            reg_compute_store<K, R, SP, AL, OFF>(job, T, x, ob, sp.full, sp.nb);
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = xn[j];
             sp = spn;
@@ -358,10 +365,15 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
             const Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
             u32x4 x[K];
             reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
-            reg_compute_store<K, R, SP, AL>(job, T, x, u.s * job.out_sstride + sp.off, sp.full, sp.nb);
+            reg_compute_store<K, R, SP, AL, OFF>(job, T, x, u.s * job.out_sstride + sp.off, sp.full, sp.nb);
             u.next(job);
         }
     }
+}
+
+template <int K, int R, int SP, bool PF, bool AL>
+__global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
+    reg_body<K, R, SP, PF, AL, 0>(job, blockIdx.x);
     // one-workgroup launches of a synchronous small call: publish completion
     // in pinned host memory (every wave's stores complete at system scope,
     // then one lane's flag store), so the host need not wait in
@@ -372,6 +384,37 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
         if (threadIdx.x == 0)
             __hip_atomic_store(job.done_flag, job.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+constexpr bool reg_prefetch(int R) { return R >= 5; }
+constexpr bool reg_argload(int K, int R) { return K * R * 5 >= 50; }
+
+// ---------------------------------------------------------------------------
+// matapply_pair<K, RA, RB>: two independent matrix applications over the same
+// k in one launch (fec_run_batch_jobs: e.g. a stripe's encode and another
+// stripe's decode), so the pair pays one launch ramp-up and drain instead of
+// two.  The grid is both jobs' grids side by side; each workgroup walks its
+// own job exactly as matapply_reg would.  RB <= min(RA, K): the second job
+// is the narrower one (a decode recovers at most k blocks).
+// ---------------------------------------------------------------------------
+template <int K, int RA, int RB>
+struct alignas(16) PairJob {
+    RegJob<K, RA> a;
+    RegJob<K, RB> b;
+    uint32_t blocks_a, pad_[3];
+};
+
+// Job a's workgroups first, then job b's: the dispatcher starts b's as a's
+// retire.  (Alternating the two jobs' workgroups measured 10 % slower on the
+// cfg2 step, profiles/r03_pair_ab.json.)
+template <int K, int RA, int RB, int SP>
+__global__ __launch_bounds__(kBlock) void matapply_pair(const PairJob<K, RA, RB> job) {
+    using PJ = PairJob<K, RA, RB>;
+    constexpr size_t kOffB = offsetof(PJ, b);
+    if (blockIdx.x < job.blocks_a)
+        reg_body<K, RA, SP, reg_prefetch(RA), reg_argload(K, RA), 0>(job.a, blockIdx.x);
+    else
+        reg_body<K, RB, SP, reg_prefetch(RB), reg_argload(K, RB), kOffB>(job.b, blockIdx.x - job.blocks_a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1111,16 +1154,11 @@ const char* const kRowsNames[kRegK + 1][kRegR + 1] = {
 // batches of many stripes, where nt sc1 measured slower (256 x 1 MiB
 // object-major 69.5 -> 67.7 %, 10^6 x 4 KiB -1 %; tools/ab_store.sh,
 // profiles/r02_store_ab.log; copy-walk probe: tools/mb_cold.exe tail).
+// Fill a register kernel's argument block for `a`; returns its grid (0: more
+// units than one launch walks -- the caller splits).  rows: matapply_rows'
+// one-wave-per-stripe walk.
 template <int K, int R>
-hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
-    // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
-    // tools/mb_encode.exe; no gain for the 3-row decode)
-    constexpr bool kPrefetch = R >= 5;
-    // more table dwords than the SGPRs hold next to the pointers: read them
-    // where they are used (K=3/M=10 encode 35.9 -> 33.6 us, tools/mb_encode.exe
-    // variant "PF AL"; the 3-row decode is unchanged either way)
-    constexpr bool kArgLoad = K * R * 5 >= 50;
-    RegJob<K, R> job;
+uint32_t fill_regjob(const ApplySpec& a, RegJob<K, R>& job, bool rows) {
     job.sz = a.sz;
     job.in_sstride = a.in_sstride;
     job.out_sstride = a.out_sstride;
@@ -1140,9 +1178,8 @@ hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
             t[3] = w[3];
             t[4] = w[4];
         }
-    const bool rows = a.sz > kRowsMin && a.sz <= kRowsMax && a.nstripes >= 64;
     const uint64_t cps = (a.sz + kChunk - 1) / kChunk;
-    if (cps * a.nstripes >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;  // the caller splits
+    if (cps * a.nstripes >= (1ull << 32) - (1ull << 24)) return 0;
     job.cps = static_cast<uint32_t>(cps);
     // one unit per lane up to the grid cap; beyond it a grid-stride loop
     const uint64_t lanes = rows ? a.nstripes * 64u : cps * a.nstripes;  // rows: one wave per stripe
@@ -1152,6 +1189,24 @@ hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
     const uint64_t gstride = uint64_t(grid) * kBlock;
     job.gs_s = static_cast<uint32_t>(gstride / cps);
     job.gs_c = static_cast<uint32_t>(gstride % cps);
+    return grid;
+}
+
+bool rows_shape(const ApplySpec& a) { return a.sz > kRowsMin && a.sz <= kRowsMax && a.nstripes >= 64; }
+
+template <int K, int R>
+hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
+    // many outputs: the prefetching walk (K=3/M=10 encode 6.17 -> 6.41 TB/s,
+    // tools/mb_encode.exe; no gain for the 3-row decode)
+    constexpr bool kPrefetch = reg_prefetch(R);
+    // more table dwords than the SGPRs hold next to the pointers: read them
+    // where they are used (K=3/M=10 encode 35.9 -> 33.6 us, tools/mb_encode.exe
+    // variant "PF AL"; the 3-row decode is unchanged either way)
+    constexpr bool kArgLoad = reg_argload(K, R);
+    RegJob<K, R> job;
+    const bool rows = rows_shape(a);
+    const uint32_t grid = fill_regjob<K, R>(a, job, rows);
+    if (!grid) return hipErrorInvalidValue;  // the caller splits
     void (*fn)(const RegJob<K, R>);
     const StorePolicy sp = config().store;
     if (rows) {
@@ -1181,6 +1236,50 @@ constexpr std::array<RegLaunch, kRegR + 1> reg_row(std::integer_sequence<int, R.
 const std::array<RegLaunch, kRegR + 1> g_reg_launch[kRegK + 1] = {
     {}, reg_row<1>(std::make_integer_sequence<int, kRegR>()), reg_row<2>(std::make_integer_sequence<int, kRegR>()),
     reg_row<3>(std::make_integer_sequence<int, kRegR>()), reg_row<4>(std::make_integer_sequence<int, kRegR>())};
+
+// ---- paired register launches (matapply_pair) ------------------------------------
+char g_pair_names[kRegK + 1][kRegR + 1][kRegR + 1][32];
+
+template <int K, int RA, int RB>
+hipError_t launch_pair(const ApplySpec& a, const ApplySpec& b, hipStream_t stream) {
+    PairJob<K, RA, RB> job;
+    const uint32_t ga = fill_regjob<K, RA>(a, job.a, false), gb = fill_regjob<K, RB>(b, job.b, false);
+    if (!ga || !gb || uint64_t(ga) + gb >= (1ull << 31)) return hipErrorNotSupported;
+    job.blocks_a = ga;
+    job.pad_[0] = job.pad_[1] = job.pad_[2] = 0;
+    // the register kernels' store policy, single-stripe (nt sc1) only when both are
+    const StorePolicy sp = config().store;
+    const bool sc1 = sp == kStoreNtSc1 || (sp == kStoreAuto && a.nstripes == 1 && b.nstripes == 1);
+    void (*fn)(const PairJob<K, RA, RB>) = sc1 ? matapply_pair<K, RA, RB, 3> : matapply_pair<K, RA, RB, 0>;
+    hipLaunchKernelGGL(fn, dim3(ga + gb), dim3(kBlock), 0, stream, job);
+    t_last_kernel = g_pair_names[K][RA][RB];
+    return hipGetLastError();
+}
+
+typedef hipError_t (*PairLaunch)(const ApplySpec&, const ApplySpec&, hipStream_t);
+typedef std::array<PairLaunch, kRegR + 1> PairRow;
+
+template <int K, int RA, int RB>
+constexpr PairLaunch pair_entry() {
+    if constexpr (RB <= K && RB <= RA)
+        return launch_pair<K, RA, RB>;
+    else
+        return nullptr;
+}
+
+template <int K, int RA, int... RB>
+constexpr PairRow pair_row(std::integer_sequence<int, RB...>) {
+    return {{nullptr, pair_entry<K, RA, RB + 1>()...}};
+}
+
+template <int K, int... RA>
+constexpr std::array<PairRow, kRegR + 1> pair_plane(std::integer_sequence<int, RA...>) {
+    return {{PairRow{}, pair_row<K, RA + 1>(std::make_integer_sequence<int, kRegR>())...}};
+}
+
+const std::array<PairRow, kRegR + 1> g_pair_launch[kRegK + 1] = {
+    {}, pair_plane<1>(std::make_integer_sequence<int, kRegR>()), pair_plane<2>(std::make_integer_sequence<int, kRegR>()),
+    pair_plane<3>(std::make_integer_sequence<int, kRegR>()), pair_plane<4>(std::make_integer_sequence<int, kRegR>())};
 
 // ---- table kernels (matapply_lds, k <= 32, r <= 48) ----------------------------
 struct LdsVariant {
@@ -1531,6 +1630,33 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);
+}
+
+hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream) {
+    std::call_once(g_dispatch_once, init_dispatch);
+    static std::once_flag names_once;
+    std::call_once(names_once, [] {
+        for (int k = 1; k <= kRegK; ++k)
+            for (int ra = 1; ra <= kRegR; ++ra)
+                for (int rb = 1; rb <= kRegR; ++rb)
+                    snprintf(g_pair_names[k][ra][rb], sizeof g_pair_names[k][ra][rb], "matapply_pair<%d,%d,%d>", k,
+                             ra, rb);
+    });
+    // the shapes launch_apply runs on matapply_reg (not matapply_rows, not a
+    // forced JIT kernel), each within one launch
+    auto reg_shape = [](const ApplySpec& a) {
+        return !a.accumulate && a.k >= 1 && a.k <= static_cast<uint32_t>(kRegK) && a.r >= 1 &&
+               a.r <= static_cast<uint32_t>(kRegR) && a.sz > 0 && a.nstripes > 0 && a.nstripes < (1ull << 32) &&
+               a.coef_stride >= a.k && !rows_shape(a);
+    };
+    if (x.k != y.k || !reg_shape(x) || !reg_shape(y) || jit_mode() == kJitForce) return hipErrorNotSupported;
+    const ApplySpec& a = x.r >= y.r ? x : y;
+    const ApplySpec& b = x.r >= y.r ? y : x;
+    const PairLaunch f = g_pair_launch[a.k][a.r][b.r];
+    if (!f) return hipErrorNotSupported;
+    t_signal_flag = nullptr;
+    t_signal_used = false;
+    return f(a, b, stream);
 }
 
 }  // namespace zfec_hip

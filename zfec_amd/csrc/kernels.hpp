@@ -61,6 +61,12 @@ struct alignas(16) MatJob {
 // shape (the caller splits it into XOR-accumulating passes).
 hipError_t launch_apply(const ApplySpec& a, hipStream_t stream);
 
+// Two independent applications over the same k in ONE launch (matapply_pair):
+// both register-kernel shapes (k <= 4, r <= 8, not matapply_rows' short
+// blocks), the narrower one's r <= k.  hipErrorNotSupported otherwise (the
+// caller launches them one at a time).  Neither may read what the other writes.
+hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream);
+
 // Whether launch_apply takes all k > kMaxIn inputs of a launch of r <= kMaxOut
 // rows, sz-byte blocks and nstripes stripes in one pass (bit-sliced kernels).
 bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes);
