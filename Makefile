@@ -80,7 +80,7 @@ build/address/libzfec_hip.so: build/address/driver
 asan-py: build/address/libzfec_hip.so
 	ASAN_OPTIONS=detect_leaks=0 LD_PRELOAD=$(ASANRT) ZFEC_HIP_LIB=$(CURDIR)/build/address/libzfec_hip.so \
 	  $(PY) -m pytest tests/test_cpu_surface.py -q -p no:cacheprovider \
-	  -k "rejects or jit_prepare or fec_new or symbols or decode_matrix or invert_vdm or enc_matrix"
+	  -k "rejects or jit_prepare or fec_new or symbols or decode_matrix or invert_vdm or enc_matrix or batch_jobs"
 
 ref:
 	$(MAKE) -C oracle ref

@@ -90,6 +90,15 @@ void check_rejects() {
             const int devs[2] = {0, 0};
             const int mst = fec_encode_batch_multi(c, a, 4, 12, o1, 4, 8, ok, 2, 4, 1, devs, 2, 0);
             CHECK(mst == FEC_ENODEV || mst == FEC_OK);
+            fec_batch_job jobs[2] = {
+                {c, FEC_JOB_ENCODE, 0, a, 4, 12, o1, 4, 8, ok, 2, 4, 1},
+                {c, FEC_JOB_DECODE, 0, a, 4, 12, o2, 4, 12, dup, 0, 4, 1},
+            };
+            const int jst = fec_run_batch_jobs(jobs, 2, nullptr, 0);
+            CHECK(jst == FEC_ENODEV || jst == FEC_EINVAL);  // no GPU here, or job 1's duplicate
+            jobs[1].kind = 9;
+            CHECK(fec_run_batch_jobs(jobs, 2, nullptr, 0) == FEC_EINVAL);
+            CHECK(std::strstr(fec_last_error_message(), "job 1: kind 9") != nullptr);
         }
         fec_free(c);
     });

@@ -267,6 +267,29 @@ def test_batch_library_errors_are_zfec_errors():
                                                                      16, 4)
 
 
+def test_batch_jobs_validation():
+    """fec_run_batch_jobs checks every job before anything runs; a failing
+    job's message names it (host logic: no GPU needed)."""
+    code = capi.Code(3, 10)
+    good = capi.encode_job(code, 0x1000, 16, 48, 0x2000, 16, 112, list(range(3, 10)), 16, 1)
+    with pytest.raises(capi.FecError, match="job 1: block number 10 out of range"):
+        capi.run_batch_jobs([good, capi.encode_job(code, 0x1000, 16, 48, 0x2000, 16, 32, [3, 10], 16, 1)])
+    with pytest.raises(capi.FecError, match="job 0: kind 7"):
+        capi.run_batch_jobs([(code, 7) + good[2:]])
+    with pytest.raises(capi.FecError, match="job 0: block_nums is NULL"):
+        arr = (capi.BatchJob * 1)(capi.BatchJob(code.ptr, capi.FEC_JOB_ENCODE, 0, 0x1000, 16, 48, 0x2000, 16, 112,
+                                                None, 7, 16, 1))
+        capi.check(capi.lib().fec_run_batch_jobs(arr, 1, None, 0))
+    assert capi.lib().fec_run_batch_jobs(None, 1, None, 0) == capi.FEC_EINVAL
+
+
+@pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")
+def test_batch_jobs_no_gpu_fails_loudly():
+    code = capi.Code(3, 10)
+    with pytest.raises(capi.FecError, match="no GPU"):
+        capi.run_batch_jobs([capi.encode_job(code, 0x1000, 16, 48, 0x2000, 16, 112, list(range(3, 10)), 16, 1)])
+
+
 _DROPIN_CHILD = r"""
 import glob, importlib.util, sys
 spec = importlib.util.spec_from_file_location("zfec_dropin._fec", sys.argv[1])

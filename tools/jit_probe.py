@@ -19,7 +19,10 @@ between variants.  Under rocprofv3 --pmc the same run gives each variant's
 counters (tools/jit_probe_pmc.sh).  Only `real` produces the code's bytes
 (checked against the table kernels on the first stripes).
 
-usage: python tools/jit_probe.py [--rounds 3] [--reps 40] [--warm 40] [--variants real,nohbm,noarith]
+usage: python tools/jit_probe.py [--shape cfg4|cfg3] [--rounds 3] [--reps 40] [--warm 40]
+                                 [--variants real,nohbm,noarith]
+(--shape cfg3: K=10/M=16, one 256 MiB stripe; launches rotate over buffer sets
+spanning >= 768 MiB so every launch reads and writes HBM, as bench.py's cold legs.)
 """
 import argparse
 import json
@@ -42,6 +45,7 @@ EXTRA_LDS = {"lds2": 40 << 10, "lds1": 100 << 10}
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="cfg4", choices=["cfg4", "cfg3"])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--warm", type=int, default=300)
@@ -49,10 +53,11 @@ def main():
     ap.add_argument("--legs-out", default=None, help="JSON of the dispatch order per variant (tools/jit_probe_summary.py)")
     ap.add_argument("--prepare-only", action="store_true", help="compile the probe kernels (no GPU) and exit")
     args = ap.parse_args()
-    k, m, ns = 20, 60, 1024
+    k, m, ns, stripe = {"cfg4": (20, 60, 1024, 1 << 20), "cfg3": (10, 16, 1, 256 << 20)}[args.shape]
     r = m - k
-    sz = -(-(1 << 20) // k)
+    sz = -(-stripe // k)
     ld = (sz + 255) // 256 * 256
+    nsets = max(1, -(-(768 << 20) // ((k + r) * ld * ns)))
     nums = list(range(k, m))
     code = capi.Code(k, m)
     names = args.variants.split(",")
@@ -65,11 +70,14 @@ def main():
         return
     capi.jit_mode(capi.JIT_FORCE)
     g = torch.Generator(device="cuda").manual_seed(20)
-    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=g)
-    zero = torch.zeros((ns, k, ld), dtype=torch.uint8, device="cuda")
-    par = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+    datas = [torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=g) for _ in range(nsets)]
+    data = datas[0]
+    zeros = [torch.zeros((ns, k, ld), dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+    pars = [torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+    par = pars[0]
     st = torch.cuda.current_stream()
-    src = [data]
+    src = [datas]
+    turn = [0]
     legs = []
 
     def leg(name, n):
@@ -79,7 +87,9 @@ def main():
             legs.append([name, n])
 
     def launch():
-        code.encode_batch(src[0].data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, nums, sz, ns,
+        i = turn[0] % nsets
+        turn[0] += 1
+        code.encode_batch(src[0][i].data_ptr(), ld, k * ld, pars[i].data_ptr(), ld, r * ld, nums, sz, ns,
                           stream=st.cuda_stream)
 
     # the real kernel's bytes against the table kernels on a few stripes
@@ -88,14 +98,16 @@ def main():
     launch()
     leg("check", 1)
     torch.cuda.synchronize()
-    want = torch.zeros((4, r, ld), dtype=torch.uint8, device="cuda")
+    nchk = min(4, ns)
+    want = torch.zeros((nchk, r, ld), dtype=torch.uint8, device="cuda")
     capi.jit_mode(capi.JIT_OFF)
     prev_g = capi.generic_mode(0)
-    code.encode_batch(data.data_ptr(), ld, k * ld, want.data_ptr(), ld, r * ld, nums, sz, 4, stream=st.cuda_stream)
+    code.encode_batch(data.data_ptr(), ld, k * ld, want.data_ptr(), ld, r * ld, nums, sz, nchk,
+                      stream=st.cuda_stream)
     torch.cuda.synchronize()
     capi.generic_mode(prev_g)
     capi.jit_mode(capi.JIT_FORCE)
-    assert torch.equal(want[:, :, :sz], par[:4, :, :sz]), "real JIT kernel != table kernel"
+    assert torch.equal(want[:, :, :sz], par[:nchk, :, :sz]), "real JIT kernel != table kernel"
 
     res = {n: [] for n in names}
     kern = {}
@@ -104,7 +116,7 @@ def main():
             os.environ["ZFEC_HIP_JIT_PROBE"] = str(PROBES[name])
             os.environ["ZFEC_HIP_JIT_LDS"] = str(EXTRA_LDS.get(name, 0))
             capi.reload_config()
-            src[0] = zero if name == "zero" else data
+            src[0] = zeros if name == "zero" else datas
             for _ in range(args.warm):
                 launch()
             leg(name + " (warm)", args.warm)
@@ -121,7 +133,8 @@ def main():
     os.environ["ZFEC_HIP_JIT_LDS"] = "0"
     capi.reload_config()
     hbm = (k + r) * sz * ns
-    out = {"shape": "K=20/M=60 encode, 1024 x 1 MiB stripes, rows %d B" % ld, "rounds": args.rounds,
+    out = {"shape": "K=%d/M=%d encode, %d x %d-byte stripes, rows %d B, %d buffer sets" % (k, m, ns, stripe, ld, nsets),
+           "rounds": args.rounds,
            "reps": args.reps, "warm": args.warm, "algorithmic_bytes_per_launch": hbm, "variants": {}}
     for name in names:
         us = res[name]

@@ -8,7 +8,7 @@ XCDs), VALU instructions per dispatch and their issue rate, and HBM bytes
 coalesced read stream).  Dispatches are paired with the variants through the
 run's --legs-out order.
 
-    python tools/jit_probe_summary.py TAG OUT.json
+    python tools/jit_probe_summary.py TAG OUT.json [cfg4|cfg3]
 """
 import csv
 import glob
@@ -58,11 +58,12 @@ def main():
     clk, n_clk, used = by_variant(os.path.join(base, "clk"), os.path.join(base, "clk_legs.json"))
     fet, _, _ = by_variant(os.path.join(base, "fetch"), os.path.join(base, "fetch_legs.json"))
     wri, _, _ = by_variant(os.path.join(base, "write"), os.path.join(base, "write_legs.json"))
-    k, m, ns = 20, 60, 1024
-    sz = -(-(1 << 20) // k)
+    shape = sys.argv[3] if len(sys.argv) > 3 else "cfg4"
+    k, m, ns, stripe = {"cfg4": (20, 60, 1024, 1 << 20), "cfg3": (10, 16, 1, 256 << 20)}[shape]
+    sz = -(-stripe // k)
     alg = (k + (m - k)) * sz * ns
     res = {"source": "tools/jit_probe_pmc.sh %s; tools/jit_probe_summary.py" % tag,
-           "shape": "K=20/M=60 encode, 1024 x 1 MiB stripes (bench cfg4), kernel %s" % (
+           "shape": "K=%d/M=%d encode, %d x %d-byte stripes (bench %s), kernel %s" % (k, m, ns, stripe, shape,
                clk.get("real", [{}])[0].get("name") if clk.get("real") else None),
            "algorithmic_bytes_per_launch": alg, "dispatches_paired": [n_clk, used],
            "clock_formula": "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass)",
