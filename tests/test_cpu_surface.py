@@ -267,6 +267,48 @@ def test_batch_library_errors_are_zfec_errors():
                                                                      16, 4)
 
 
+@pytest.mark.skipif(zfec_amd.device_count() > 0, reason="bogus addresses: only without a GPU")
+def test_batch_call_matches_ctypes_binding():
+    """capi's batched calls go through zfec_amd._fec.batch_call (the C-ABI
+    called from C); the ctypes binding of the same functions must report the
+    same statuses and messages for the same arguments (host-side validation:
+    no GPU needed)."""
+    from zfec_amd import _fec
+
+    capi.lib()
+    assert capi._batch_call is _fec.batch_call
+    code = capi.Code(3, 10)
+    L = capi.lib()
+    cases = [
+        # (kind, src, sbs, sss, dst, dbs, dss, nums, sz, ns)
+        (0, 0x1000, 16, 48, 0x2000, 16, 112, [3, 10], 16, 1),  # block number out of range
+        (1, 0x1000, 16, 48, 0x2000, 16, 48, [3, 3, 4], 16, 1),  # duplicate
+        (1, 0x1000, 16, 48, 0x2000, 16, 48, [1, 0, 5], 16, 1),  # misplaced primary
+        (1, 0x1000, 16, 48, 0x2000, 16, 48, [3, 4], 16, 1),  # too few slot numbers
+        (0, 0, 16, 48, 0x2000, 16, 112, [3, 4], 16, 1),  # NULL source
+    ]
+    for kind, src, sbs, sss, dst, dbs, dss, nums, sz, ns in cases:
+        st_fast = _fec.batch_call(kind, code.ptr, src, sbs, sss, dst, dbs, dss, nums, sz, ns, 0, capi.FEC_FLAG_ASYNC)
+        msg_fast = L.fec_last_error_message()
+        arr = capi.uint_array(list(nums) + [0xFFFFFFFF] * (3 - len(nums)) if kind else nums)
+        if kind == 0:
+            st_ct = L.fec_encode_batch(code.ptr, src, sbs, sss, dst, dbs, dss, arr, len(nums), sz, ns, None,
+                                       capi.FEC_FLAG_ASYNC)
+        else:
+            st_ct = L.fec_decode_batch(code.ptr, src, sbs, sss, dst, dbs, dss, arr, sz, ns, None,
+                                       capi.FEC_FLAG_ASYNC)
+        assert (st_fast, msg_fast) == (st_ct, L.fec_last_error_message()), (kind, nums)
+        assert st_fast != capi.FEC_OK
+    with pytest.raises(TypeError):
+        _fec.batch_call(0, code.ptr)
+    with pytest.raises(zfec_amd.Error, match="at most 256"):
+        _fec.batch_call(0, code.ptr, 1, 1, 1, 1, 1, 1, list(range(257)), 1, 1, 0, 0)
+    with pytest.raises(OverflowError):
+        _fec.batch_call(0, code.ptr, -1, 1, 1, 1, 1, 1, [3], 1, 1, 0, 0)
+    with pytest.raises(TypeError):
+        _fec.batch_call(0, code.ptr, 1, 1, 1, 1, 1, 1, 3, 1, 1, 0, 0)
+
+
 def test_batch_jobs_validation():
     """fec_run_batch_jobs checks every job before anything runs; a failing
     job's message names it (host logic: no GPU needed)."""

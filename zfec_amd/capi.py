@@ -71,10 +71,15 @@ class FecT(ctypes.Structure):
 
 
 _lib = None
+# zfec_amd._fec.batch_call: the batched entry points called from C (the ctypes
+# conversion of their thirteen arguments is ~2 us of host cost per call).  Only
+# with the in-tree library, which the extension links: with ZFEC_HIP_LIB set
+# (another build) every call stays on that library through ctypes.
+_batch_call = None
 
 
 def lib():
-    global _lib
+    global _lib, _batch_call
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError("libzfec_hip.so is not built (run `make` or __graft_entry__.build())")
@@ -88,6 +93,12 @@ def lib():
             f.argtypes = args
         L.fec_init()
         _lib = L
+        if not os.environ.get("ZFEC_HIP_LIB") and not os.environ.get("ZFEC_CAPI_CTYPES"):
+            try:
+                from . import _fec
+            except ImportError:
+                _fec = None
+            _batch_call = getattr(_fec, "batch_call", None)
     return _lib
 
 
@@ -187,12 +198,22 @@ class Code(object):
         check(lib().fec_jit_prepare_decode(self.ptr, uint_array(index), flags))
 
     def encode_batch(self, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
+        if _batch_call is not None:
+            st = _batch_call(0, self.ptr, src, sbs, sss, dst, dbs, dss, block_nums, sz, nstripes, stream or 0, flags)
+            if st:
+                check(st)
+            return
         st = _lib.fec_encode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, _nums(block_nums), len(block_nums), sz,
                                    nstripes, stream or None, flags)
         if st:
             check(st)
 
     def decode_batch(self, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, stream=0, flags=FEC_FLAG_ASYNC):
+        if _batch_call is not None:
+            st = _batch_call(1, self.ptr, src, sbs, sss, dst, dbs, dss, index, sz, nstripes, stream or 0, flags)
+            if st:
+                check(st)
+            return
         st = _lib.fec_decode_batch(self.ptr, src, sbs, sss, dst, dbs, dss, _nums(index), sz, nstripes,
                                    stream or None, flags)
         if st:

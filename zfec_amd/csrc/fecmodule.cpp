@@ -581,6 +581,64 @@ PyObject* test_from_agl(PyObject*, PyObject*) {
     Py_RETURN_FALSE;
 }
 
+// batch_call(kind, code, src, sbs, sss, dst, dbs, dss, nums, sz, nstripes, stream, flags) -> status
+//
+// fec_encode_batch (kind 0) / fec_decode_batch (kind 1) of the C-ABI, called
+// from C: `code` is a fec_t* from fec_new, buffers and the stream are raw
+// addresses, `nums` a tuple or list of block numbers (decode: the k slot
+// numbers).  Returns the call's status (fec_last_error_message holds the
+// message).  zfec_amd.capi routes its batched calls here: ctypes' conversion
+// of the thirteen arguments cost ~2 us of the ~5 us host enqueue of a batched
+// launch (BENCH_r02 host_enqueue_us 5.1 vs 3.2 from C, tools/host_cost.hip).
+PyObject* py_batch_call(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+    if (nargs != 13) {
+        PyErr_Format(PyExc_TypeError, "batch_call takes 13 arguments (%zd given)", nargs);
+        return nullptr;
+    }
+    size_t v[13] = {};
+    for (int i = 0; i < 13; ++i) {
+        if (i == 8) continue;
+        v[i] = PyLong_AsSize_t(args[i]);
+        if (v[i] == size_t(-1) && PyErr_Occurred()) return nullptr;
+    }
+    PyObject* seq = PySequence_Fast(args[8], "batch_call: nums must be a tuple or list");
+    if (!seq) return nullptr;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    unsigned nums[256];
+    if (n > 256) {
+        Py_DECREF(seq);
+        PyErr_SetString(py_fec_error, "Precondition violation: at most 256 block numbers");
+        return nullptr;
+    }
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        const unsigned long x = PyLong_AsUnsignedLong(PySequence_Fast_GET_ITEM(seq, i));
+        if (x == static_cast<unsigned long>(-1) && PyErr_Occurred()) {
+            Py_DECREF(seq);
+            return nullptr;
+        }
+        nums[i] = x > 0xffffffffu ? 0xffffffffu : static_cast<unsigned>(x);  // out of range: the library rejects it
+    }
+    Py_DECREF(seq);
+    // decode reads k slot numbers: missing ones are out of range (rejected)
+    for (Py_ssize_t i = n; i < 256; ++i) nums[i] = 0xffffffffu;
+    const fec_t* code = reinterpret_cast<const fec_t*>(v[1]);
+    const gf* src = reinterpret_cast<const gf*>(v[2]);
+    gf* dst = reinterpret_cast<gf*>(v[5]);
+    void* stream = reinterpret_cast<void*>(v[11]);
+    const unsigned flags = static_cast<unsigned>(v[12]);
+    int st;
+    if (v[0] == 0) {
+        Py_BEGIN_ALLOW_THREADS st = fec_encode_batch(code, src, v[3], v[4], dst, v[6], v[7], nums, size_t(n), v[9],
+                                                     v[10], stream, flags);
+        Py_END_ALLOW_THREADS
+    } else {
+        Py_BEGIN_ALLOW_THREADS st = fec_decode_batch(code, src, v[3], v[4], dst, v[6], v[7], nums, v[9], v[10],
+                                                     stream, flags);
+        Py_END_ALLOW_THREADS
+    }
+    return PyLong_FromLong(st);
+}
+
 PyObject* py_device_count(PyObject*, PyObject*) { return PyLong_FromLong(fec_device_count()); }
 PyObject* py_version(PyObject*, PyObject*) { return PyUnicode_FromString(fec_version()); }
 
@@ -588,6 +646,9 @@ PyMethodDef module_functions[] = {
     {"test_from_agl", test_from_agl, METH_NOARGS, "Encode/decode round trip of zfec's C self-test (on the GPU)."},
     {"device_count", py_device_count, METH_NOARGS, "Number of visible GPUs."},
     {"version", py_version, METH_NOARGS, "Library version."},
+    {"batch_call", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_batch_call)), METH_FASTCALL,
+     "batch_call(kind, code, src, sbs, sss, dst, dbs, dss, nums, sz, nstripes, stream, flags) -> status: "
+     "fec_encode_batch (kind 0) / fec_decode_batch (kind 1) with raw addresses."},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moduledef = {PyModuleDef_HEAD_INIT, "_fec", "FEC - Forward Error Correction on MI355X", -1,
