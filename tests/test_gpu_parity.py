@@ -1144,3 +1144,53 @@ def test_small_call_wait_modes(mode, knobs):
             rec = dec.decode([out[7], out[1], out[9]], [7, 1, 9])
             assert capi.last_wait() == (1 if mode == "signal" else 0), (mode, sz)
             assert b"".join(rec) == data.tobytes(), sz
+
+
+def test_small_call_signal_under_load():
+    """The completion word a one-workgroup small call publishes must never
+    overtake its output bytes (kernels.hip matapply_reg: every wave waits for
+    its stores, barrier, one lane's system-scope release, then the flag).
+    2000 synchronous 4 KiB K=3/M=10 encodes and decodes from bytes, each
+    checked against the oracle, while another thread keeps the GPU busy with
+    large device-resident encodes on its own stream (MI355X_MICROARCH.md:
+    test hand-offs under uneven load)."""
+    import threading
+
+    import torch
+
+    k, m = 3, 10
+    stop = threading.Event()
+    errors = []
+
+    def load():
+        try:
+            code = capi.Code(20, 60)
+            st = torch.cuda.Stream()
+            ld = 1 << 20
+            src = torch.randint(0, 256, (8, 20, ld), dtype=torch.uint8, device="cuda")
+            dst = torch.empty((8, 40, ld), dtype=torch.uint8, device="cuda")
+            while not stop.is_set():
+                code.encode_batch(src.data_ptr(), ld, 20 * ld, dst.data_ptr(), ld, 40 * ld, list(range(20, 60)),
+                                  ld, 8, stream=st.cuda_stream)
+                st.synchronize()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = threading.Thread(target=load)
+    th.start()
+    try:
+        rng = np.random.default_rng(2000)
+        enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+        for i in range(2000):
+            sz = 1366 if i % 3 else int(rng.integers(1, 4097))
+            data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+            out = enc.encode([data[j].tobytes() for j in range(k)])
+            assert capi.last_wait() == 1
+            par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+            assert (par == oracle.encode(k, m, data)).all(), (i, sz)
+            rec = dec.decode([out[7], out[8], out[9]], [7, 8, 9])
+            assert b"".join(rec) == data.tobytes(), (i, sz)
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors

@@ -117,6 +117,25 @@ int main() {
     printf("  fec_encode_ex 3->7         %6.2f\n",
            per_call_us([&] { fec_encode_ex(code, in, out, nums, 7, sz, st, FEC_FLAG_ASYNC); }));
     printf("  last status %d (%s), kernel %s\n", fec_last_status(), fec_last_error_message(), fec_last_kernel_name());
+    {
+        // synchronous small calls from pageable host memory, launch to return:
+        // the Python bytes API's 4 KiB K=3/M=10 stripe (sz = 1366) without Python
+        const size_t hs = 1366;
+        std::vector<unsigned char> h(10 * hs, 7);
+        const gf* hin[3] = {&h[0], &h[hs], &h[2 * hs]};
+        gf* hout[7];
+        for (int i = 0; i < 7; ++i) hout[i] = &h[(3 + i) * hs];
+        printf("  sync 4 KiB encode, host, FEC_FLAG_HOST_MEMORY %6.2f\n",
+               per_call_us([&] { fec_encode_ex(code, hin, hout, nums, 7, hs, nullptr, FEC_FLAG_HOST_MEMORY); }, 5000));
+        printf("  sync 4 KiB encode, host, classified           %6.2f\n",
+               per_call_us([&] { fec_encode(code, hin, hout, nums, 7, hs); }, 5000));
+        const gf* dinb[3] = {hout[4], hout[5], hout[6]};
+        gf* doutb[3] = {&h[0], &h[hs], &h[2 * hs]};
+        printf("  sync 4 KiB decode 3->3, host, FEC_FLAG_HOST_MEMORY %6.2f\n",
+               per_call_us([&] { fec_decode_ex(code, dinb, doutb, slots, hs, nullptr, FEC_FLAG_HOST_MEMORY); }, 5000));
+        printf("  last status %d (%s), kernel %s, signal wait %d\n", fec_last_status(), fec_last_error_message(),
+               fec_last_kernel_name(), fec_last_wait());
+    }
     fec_free(code);
     return 0;
 }

@@ -185,14 +185,9 @@ def _capi_code(coder):
 class Encoder(_fec.Encoder):
     """Encoder(k, m) -- see zfec/_fecmodule.c:40-44."""
 
-    def encode(self, inblocks, desired_blocks_nums=None):
-        try:
-            first = inblocks[0]
-        except Exception:
-            first = None
-        if first is None or not _is_device_tensor(first):
-            return _fec.Encoder.encode(self, inblocks, desired_blocks_nums)
-        return self._encode_device(list(inblocks), desired_blocks_nums)
+    # encode(inblocks, desired_blocks_nums=None) is _fec.Encoder.encode: host
+    # buffers run in C; device tensors come back to _encode_device
+    # (fecmodule.cpp route_device)
 
     def encode_batch(self, blocks, desired_blocks_nums=None, devices=None):
         """Encode many independent stripes in one launch (fec_encode_batch).
@@ -237,6 +232,7 @@ class Encoder(_fec.Encoder):
     def _encode_device(self, inblocks, desired):
         import torch
 
+        inblocks = list(inblocks)
         k, m = self.k, self.m
         if desired is None:
             nums = list(range(m))
@@ -267,14 +263,8 @@ class Encoder(_fec.Encoder):
 class Decoder(_fec.Decoder):
     """Decoder(k, m) -- see zfec/_fecmodule.c:321-325."""
 
-    def decode(self, blocks, blocknums):
-        try:
-            first = blocks[0]
-        except Exception:
-            first = None
-        if first is None or not _is_device_tensor(first):
-            return _fec.Decoder.decode(self, blocks, blocknums)
-        return self._decode_device(list(blocks), blocknums)
+    # decode(blocks, blocknums) is _fec.Decoder.decode; device tensors come
+    # back to _decode_device (fecmodule.cpp route_device)
 
     def decode_batch(self, blocks, blocknums, devices=None):
         """Decode many independent stripes that all received the same block
@@ -346,6 +336,7 @@ class Decoder(_fec.Decoder):
         return nums
 
     def _decode_device(self, blocks, blocknums):
+        blocks = list(blocks)
         import torch
 
         k = self.k

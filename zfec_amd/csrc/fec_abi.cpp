@@ -850,6 +850,11 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // them zero-copy (A/B runs).
     const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide;
     bool signalled = false;
+    // Every block in the bounce buffer: its slots are 256-byte multiples, so
+    // the kernel may run each row out to its next 128-byte line (whole 16-byte
+    // units, no byte-wise tail: over PCIe each tail byte load is a round trip
+    // of its own); the bytes past sz are never copied out.
+    const size_t ksz = nhost == size_t(k) + r ? std::min(slot, align_up(sz, 128)) : sz;
     if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
@@ -859,7 +864,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         if (k <= 4 && r <= 8 && sz <= 4096)
             if (uint32_t* f = signal_slot(*d)) matapply_request_signal(f, d->seq);
         const unsigned launches0 = t_launches;
-        const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st);
+        const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), ksz, 1, 0, 0, st);
         // the kernel's signal covers the call only if it was its one launch
         signalled = st0 == FEC_OK && matapply_signal_used() && t_launches - launches0 == 1;
         matapply_request_signal(nullptr, 0);  // an unconsumed request must not reach a later launch
@@ -871,7 +876,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = base + slot * (nin + q);
         if (nin && (e = hipMemcpyAsync(base, hb, slot * nin, hipMemcpyHostToDevice, st)) != hipSuccess)
             return hip_fail(e, "hipMemcpyAsync H2D");
-        if (apply_matrix(coef, k, r, m.din.data(), m.dout.data(), sz, 1, 0, 0, st)) return t_status;
+        if (apply_matrix(coef, k, r, m.din.data(), m.dout.data(), ksz, 1, 0, 0, st)) return t_status;
         if (nout && (e = hipMemcpyAsync(hb + slot * nin, base + slot * nin, slot * nout, hipMemcpyDeviceToHost,
                                         st)) != hipSuccess)
             return hip_fail(e, "hipMemcpyAsync D2H");

@@ -19,6 +19,7 @@
 
 #include <malloc.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -131,15 +132,18 @@ bool ready(Coder* self) {
     return true;
 }
 
-// Holds acquired buffers and releases them on scope exit.
+// Holds acquired buffers (at most 256: k <= 256) and releases them on scope
+// exit.  Fixed arrays on the stack here and below: a small call's host cost
+// is counted in microseconds, and growing vectors cost a dozen allocations.
 struct Buffers {
-    std::vector<Py_buffer> v;
-    explicit Buffers(size_t n) : v(n) {
-        for (auto& b : v) b.obj = nullptr;
+    Py_buffer v[256];
+    size_t n;
+    explicit Buffers(size_t cnt) : n(cnt) {
+        for (size_t i = 0; i < n; ++i) v[i].obj = nullptr;
     }
     ~Buffers() {
-        for (auto& b : v)
-            if (b.obj) PyBuffer_Release(&b);
+        for (size_t i = 0; i < n; ++i)
+            if (v[i].obj) PyBuffer_Release(&v[i]);
     }
 };
 
@@ -164,6 +168,35 @@ int raise_status(int st) {
     return -1;
 }
 
+// zfec_amd.Encoder / Decoder (the Python subclasses) take device tensors too:
+// a first block with no buffer protocol whose .is_cuda is true routes the
+// call to the subclass's _encode_device / _decode_device.  Checked here
+// rather than in a Python override of encode/decode, so a call on bytes
+// enters C directly (one Python frame less per small call).  Returns 1 with
+// the result in *out, 0 if not routed, -1 with an exception set.
+int route_device(PyObject* self, PyObject* blocks, const char* method, PyObject* a2, PyObject** out) {
+    if (!PyObject_HasAttrString(self, method)) return 0;  // the bare _fec type
+    PyObject* first = PySequence_Check(blocks) ? PySequence_GetItem(blocks, 0) : nullptr;
+    if (!first) {
+        PyErr_Clear();
+        return 0;
+    }
+    int routed = 0;
+    if (!PyObject_CheckBuffer(first)) {
+        PyObject* cuda = PyObject_GetAttrString(first, "is_cuda");
+        if (!cuda) {
+            PyErr_Clear();
+        } else {
+            routed = PyObject_IsTrue(cuda) == 1;
+            Py_DECREF(cuda);
+        }
+    }
+    Py_DECREF(first);
+    if (!routed) return 0;
+    *out = PyObject_CallMethod(self, method, "OO", blocks, a2 ? a2 : Py_None);
+    return *out ? 1 : -1;
+}
+
 // ---- Encoder.encode -----------------------------------------------------------
 // zfec/_fecmodule.c:116-260
 PyObject* Encoder_encode(Coder* self, PyObject* args) {
@@ -171,9 +204,15 @@ PyObject* Encoder_encode(Coder* self, PyObject* args) {
     PyObject* desired = nullptr;
     if (!PyArg_ParseTuple(args, "O|O:Encoder.encode", &inblocks, &desired)) return nullptr;
     if (!ready(self)) return nullptr;
+    {
+        PyObject* routed = nullptr;
+        const int rd = route_device(reinterpret_cast<PyObject*>(self), inblocks, "_encode_device", desired, &routed);
+        if (rd) return rd > 0 ? routed : nullptr;
+    }
     const unsigned k = self->kk, m = self->mm;
 
-    std::vector<long> nums;
+    thread_local std::vector<long> nums;  // reused: no allocation per call
+    nums.clear();
     if (desired && desired != Py_None) {
         PyObject* fd = PySequence_Fast(desired, "Second argument (optional) was not a sequence.");
         if (!fd) return nullptr;
@@ -205,7 +244,7 @@ PyObject* Encoder_encode(Coder* self, PyObject* args) {
     }
     PyObject** items = PySequence_Fast_ITEMS(fast);
     Buffers bufs(k);
-    std::vector<const gf*> in(k);
+    const gf* in[256];
     Py_ssize_t sz = -1;
     for (unsigned i = 0; i < k; ++i) {
         if (PyObject_GetBuffer(items[i], &bufs.v[i], PyBUF_SIMPLE)) {
@@ -233,36 +272,53 @@ PyObject* Encoder_encode(Coder* self, PyObject* args) {
 
     // one fresh bytes object per requested secondary block (_fecmodule.c:206-217)
     reuse_freed_outputs(sz);
-    std::vector<unsigned> ids;
-    std::vector<PyObject*> produced;
-    std::vector<gf*> outp;
+    // desired numbers may repeat (the reference allows it): up to nums.size() outputs
+    std::vector<unsigned> ids_big;
+    std::vector<PyObject*> produced_big;
+    std::vector<gf*> outp_big;
+    unsigned ids_s[256];
+    PyObject* produced_s[256];
+    gf* outp_s[256];
+    unsigned* ids = ids_s;
+    PyObject** produced = produced_s;
+    gf** outp = outp_s;
+    if (nums.size() > 256) {
+        ids_big.resize(nums.size());
+        produced_big.resize(nums.size());
+        outp_big.resize(nums.size());
+        ids = ids_big.data();
+        produced = produced_big.data();
+        outp = outp_big.data();
+    }
+    size_t nout = 0;
     for (long x : nums)
         if (x >= static_cast<long>(k)) {
             PyObject* b = PyBytes_FromStringAndSize(nullptr, sz);
             if (!b) {
-                for (PyObject* o : produced) Py_DECREF(o);
+                for (size_t i = 0; i < nout; ++i) Py_DECREF(produced[i]);
                 Py_DECREF(fast);
                 return nullptr;
             }
-            ids.push_back(static_cast<unsigned>(x));
-            produced.push_back(b);
-            outp.push_back(reinterpret_cast<gf*>(PyBytes_AS_STRING(b)));
+            ids[nout] = static_cast<unsigned>(x);
+            produced[nout] = b;
+            outp[nout] = reinterpret_cast<gf*>(PyBytes_AS_STRING(b));
+            ++nout;
         }
     int st = FEC_OK;
-    if (!ids.empty()) {
-        Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, in.data(), outp.data(), ids.data(), ids.size(),
-                                                  static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
+    if (nout) {
+        Py_BEGIN_ALLOW_THREADS st = fec_encode_ex(self->fec_matrix, in, outp, ids, nout, static_cast<size_t>(sz), nullptr,
+                                                  FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
-        for (PyObject* o : produced) Py_DECREF(o);
+        for (size_t i = 0; i < nout; ++i) Py_DECREF(produced[i]);
         Py_DECREF(fast);
         raise_status(st);
         return nullptr;
     }
     PyObject* result = PyList_New(static_cast<Py_ssize_t>(nums.size()));
     if (!result) {
-        for (PyObject* o : produced) Py_DECREF(o);
+        for (size_t i = 0; i < nout; ++i) Py_DECREF(produced[i]);
         Py_DECREF(fast);
         return nullptr;
     }
@@ -286,6 +342,11 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
     PyObject *blocks, *blocknums;
     if (!PyArg_ParseTuple(args, "OO:Decoder.decode", &blocks, &blocknums)) return nullptr;
     if (!ready(self)) return nullptr;
+    {
+        PyObject* routed = nullptr;
+        const int rd = route_device(reinterpret_cast<PyObject*>(self), blocks, "_decode_device", blocknums, &routed);
+        if (rd) return rd > 0 ? routed : nullptr;
+    }
     const unsigned k = self->kk, m = self->mm;
 
     PyObject* fb = PySequence_Fast(blocks, "First argument was not a sequence.");
@@ -317,9 +378,9 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
                      PySequence_Fast_GET_SIZE(fn), int(k));
         return nullptr;
     }
-    std::vector<long> nums;
+    thread_local std::vector<long> nums;  // reused: no allocation per call
     if (!parse_nums(fn, nums)) return nullptr;
-    std::vector<unsigned char> seen(256, 0);
+    unsigned char seen[256] = {};
     for (long x : nums) {
         if (x < 0 || x > 255) {  // _fecmodule.c:459-462
             PyErr_Format(py_fec_error,
@@ -340,9 +401,10 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
     }
     PyObject** items = PySequence_Fast_ITEMS(fb);
     Buffers bufs(k);
-    std::vector<const gf*> cblocks(k);
-    std::vector<PyObject*> objs(items, items + k);
-    std::vector<unsigned> cnums(k);
+    const gf* cblocks[256];
+    PyObject* objs[256];
+    unsigned cnums[256];
+    std::copy(items, items + k, objs);
     Py_ssize_t sz = -1;
     for (unsigned i = 0; i < k; ++i) {
         if (PyObject_GetBuffer(items[i], &bufs.v[i], PyBUF_SIMPLE)) {
@@ -376,33 +438,34 @@ PyObject* Decoder_decode(Coder* self, PyObject* args) {
             std::swap(objs[i], objs[c]);
         }
     }
-    std::vector<PyObject*> rec;
-    std::vector<gf*> recp;
+    PyObject* rec[256];
+    gf* recp[256];
+    size_t nrec = 0;
     reuse_freed_outputs(sz);
     for (unsigned i = 0; i < k; ++i)
         if (cnums[i] >= k) {
             PyObject* b = PyBytes_FromStringAndSize(nullptr, sz);
             if (!b) {
-                for (PyObject* o : rec) Py_DECREF(o);
+                for (size_t q = 0; q < nrec; ++q) Py_DECREF(rec[q]);
                 return nullptr;
             }
-            rec.push_back(b);
-            recp.push_back(reinterpret_cast<gf*>(PyBytes_AS_STRING(b)));
+            rec[nrec] = b;
+            recp[nrec++] = reinterpret_cast<gf*>(PyBytes_AS_STRING(b));
         }
     int st = FEC_OK;
-    if (!rec.empty()) {
-        Py_BEGIN_ALLOW_THREADS st =
-            fec_decode_ex(self->fec_matrix, cblocks.data(), recp.data(), cnums.data(), static_cast<size_t>(sz), nullptr, FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
+    if (nrec) {
+        Py_BEGIN_ALLOW_THREADS st = fec_decode_ex(self->fec_matrix, cblocks, recp, cnums, static_cast<size_t>(sz), nullptr,
+                                                  FEC_FLAG_LIBRARY_STREAM | FEC_FLAG_HOST_MEMORY);
         Py_END_ALLOW_THREADS
     }
     if (st != FEC_OK) {
-        for (PyObject* o : rec) Py_DECREF(o);
+        for (size_t q = 0; q < nrec; ++q) Py_DECREF(rec[q]);
         raise_status(st);
         return nullptr;
     }
     PyObject* result = PyList_New(k);
     if (!result) {
-        for (PyObject* o : rec) Py_DECREF(o);
+        for (size_t q = 0; q < nrec; ++q) Py_DECREF(rec[q]);
         return nullptr;
     }
     size_t ri = 0;

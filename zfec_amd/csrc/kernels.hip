@@ -375,14 +375,22 @@ template <int K, int R, int SP, bool PF, bool AL>
 __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
     reg_body<K, R, SP, PF, AL, 0>(job, blockIdx.x);
     // one-workgroup launches of a synchronous small call: publish completion
-    // in pinned host memory (every wave's stores complete at system scope,
-    // then one lane's flag store), so the host need not wait in
-    // hipStreamSynchronize (fec_abi.cpp run_single)
+    // in pinned host memory, so the host need not wait in
+    // hipStreamSynchronize (fec_abi.cpp run_single).  Every storing wave waits
+    // for its own stores, the workgroup meets at a barrier, and ONE lane
+    // releases at system scope and stores the flag (MI355X_MICROARCH.md
+    // "Valid forms"): one L2 write-back per call.  (A system fence in every
+    // wave before the barrier, round 2's form, cost five write-backs: the
+    // kernel took 6.1 us in the trace against 2.6 us for this form,
+    // tools/inline_probe.hip, profiles/r03_small_call_kernels.txt.)
     if (job.done_flag) {
-        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(job.done_flag, job.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(job.done_flag, job.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
