@@ -1194,3 +1194,25 @@ def test_small_call_signal_under_load():
         stop.set()
         th.join()
     assert not errors, errors
+
+
+def test_small_call_compact_kernel():
+    """Synchronous calls from bytes with k <= 4, r <= 8 and blocks of at most
+    4 KiB run on the compact one-workgroup kernel (kernels.hip matapply_one,
+    whole 16-byte units in the bounce buffer): bit-exact against the oracle
+    for every such (k, r) at sizes around the unit and the 4 KiB limit; one
+    byte past the limit takes the general kernels."""
+    rng = np.random.default_rng(77)
+    for k in range(1, 5):
+        for m in range(k + 1, k + 9):
+            enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+            for sz in (1, 15, 16, 17, 1366, 4095, 4096, 4097):
+                data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+                out = enc.encode([data[i].tobytes() for i in range(k)])
+                name = capi.last_kernel_name()
+                assert (name == "matapply_one<%d>" % k) == (sz <= 4096), (k, m, sz, name)
+                par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+                assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+                nums = list(range(m - k, m))
+                rec = dec.decode([out[i] for i in nums], nums)
+                assert b"".join(rec) == data.tobytes(), (k, m, sz)

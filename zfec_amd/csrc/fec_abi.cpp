@@ -859,16 +859,37 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = hbd + slot * (nin + q);
-        // one launch of at most one workgroup (k <= 4, r <= 8, sz <= 4 KiB): it
-        // signals its own completion
-        if (k <= 4 && r <= 8 && sz <= 4096)
-            if (uint32_t* f = signal_slot(*d)) matapply_request_signal(f, d->seq);
-        const unsigned launches0 = t_launches;
-        const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), ksz, 1, 0, 0, st);
-        // the kernel's signal covers the call only if it was its one launch
-        signalled = st0 == FEC_OK && matapply_signal_used() && t_launches - launches0 == 1;
-        matapply_request_signal(nullptr, 0);  // an unconsumed request must not reach a later launch
-        if (st0) return t_status;
+        if (k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && cfg.small_one) {
+            // whole 16-byte units in one workgroup: the compact kernel
+            // (kernels.hip matapply_one), which signals its own completion
+            uint32_t* f = signal_slot(*d);
+            ApplySpec a;
+            a.coef = coef;
+            a.coef_stride = k;
+            a.k = k;
+            a.r = r;
+            a.in = m.din.data();
+            a.out = m.dout.data();
+            a.sz = ksz;
+            a.nstripes = 1;
+            a.in_sstride = a.out_sstride = 0;
+            a.accumulate = false;
+            ++t_launches;
+            const hipError_t le = launch_one(a, st, f, f ? d->seq : 0);
+            if (le != hipSuccess) return hip_fail(le, "launch_one");
+            signalled = f != nullptr;
+        } else {
+            // one launch of at most one workgroup (k <= 4, r <= 8, sz <= 4 KiB): it
+            // signals its own completion
+            if (k <= 4 && r <= 8 && sz <= 4096)
+                if (uint32_t* f = signal_slot(*d)) matapply_request_signal(f, d->seq);
+            const unsigned launches0 = t_launches;
+            const int st0 = apply_matrix(coef, k, r, m.din.data(), m.dout.data(), ksz, 1, 0, 0, st);
+            // the kernel's signal covers the call only if it was its one launch
+            signalled = st0 == FEC_OK && matapply_signal_used() && t_launches - launches0 == 1;
+            matapply_request_signal(nullptr, 0);  // an unconsumed request must not reach a later launch
+            if (st0) return t_status;
+        }
     } else {
         if (ensure_dbuf(*d, slot * nhost)) return t_status;
         uint8_t* base = static_cast<uint8_t*>(d->dbuf);

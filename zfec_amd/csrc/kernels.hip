@@ -394,6 +394,80 @@ __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// matapply_one<K>: the synchronous small call from host memory (fec_abi.cpp
+// run_single: every block in the thread's pinned bounce buffer, read and
+// written over PCIe).  One workgroup, one whole 16-byte unit per lane (the
+// bounce buffer's 256-byte slots let a row run to its 16-byte multiple), and
+// the output rows in a loop that is not unrolled, each row's tables and
+// pointer read from the argument segment where they are used.  A
+// one-workgroup launch lands on any XCD and fetches its instructions cold, so
+// code size is latency: matapply_reg<3,7> (7.4 KB of code, the unrolled rows
+// and the grid-stride walk with its prefetch and tail paths) took 5.5 us in
+// the kernel trace against 2.6 us for a stand-in of the same PCIe traffic
+// (profiles/r03_small_call_kernels.txt).
+// ---------------------------------------------------------------------------
+struct alignas(16) OneJob {
+    const uint8_t* in[4];
+    uint8_t* out[8];
+    uint32_t* done_flag;
+    uint32_t units, r, done_seq, pad_;
+    uint32_t tab[4 * 8 * 5];  // row-major (r, j) coefficient tables, K per row
+};
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void matapply_one(const OneJob job) {
+    // the coefficient tables (up to 160 dwords) reach LDS in ONE vector load
+    // round trip (a lane per 16 bytes of the argument segment), not in a
+    // chain of scalar loads per output row
+    __shared__ u32x4 stab[4 * 8 * 5 / 4];
+    const uint32_t u = threadIdx.x;
+    const uint32_t ntab4 = (job.r * K * 5 + 3) / 4;
+    if (u < ntab4) {
+        const KPtr<OneJob> kj = kernarg_job<OneJob>();
+        stab[u] = reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(kj->tab)[u];
+    }
+    u32x4 x[K];
+    if (u < job.units) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + size_t(u) * 16);
+    }
+    __syncthreads();
+    if (u < job.units) {
+        Sel sel[4][K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            sel[0][j] = selectors(x[j].x);
+            sel[1][j] = selectors(x[j].y);
+            sel[2][j] = selectors(x[j].z);
+            sel[3][j] = selectors(x[j].w);
+        }
+        const uint32_t* st = reinterpret_cast<const uint32_t*>(stab);
+#pragma unroll 1
+        for (uint32_t r = 0; r < job.r; ++r) {
+            Tab t[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t i = (r * K + j) * 5;
+                t[j] = Tab{st[i], st[i + 1], st[i + 2], st[i + 3], st[i + 4]};
+            }
+            const u32x4 y{gf_dot<K>(t, sel[0]), gf_dot<K>(t, sel[1]), gf_dot<K>(t, sel[2]), gf_dot<K>(t, sel[3])};
+            store16_pol<3>(job.out[r] + size_t(u) * 16, y);
+        }
+    }
+    // completion as matapply_reg's: every wave waits for its stores, barrier,
+    // one lane's system-scope release, then the flag
+    if (job.done_flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(job.done_flag, job.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 constexpr bool reg_prefetch(int R) { return R >= 5; }
 constexpr bool reg_argload(int K, int R) { return K * R * 5 >= 50; }
 
@@ -1638,6 +1712,34 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);
+}
+
+hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq) {
+    static const char* const kOneNames[5] = {"", "matapply_one<1>", "matapply_one<2>", "matapply_one<3>",
+                                             "matapply_one<4>"};
+    if (a.k < 1 || a.k > 4 || a.r < 1 || a.r > 8 || a.nstripes != 1 || a.sz == 0 || a.sz % 16 || a.sz > 4096 ||
+        a.accumulate || a.coef_stride < a.k)
+        return hipErrorInvalidValue;
+    t_signal_flag = nullptr;  // an unconsumed launch_apply request must not outlive this launch
+    t_signal_used = false;
+    OneJob job;
+    std::memset(&job, 0, sizeof job);
+    for (uint32_t j = 0; j < a.k; ++j) job.in[j] = a.in[j];
+    for (uint32_t i = 0; i < a.r; ++i) job.out[i] = a.out[i];
+    job.done_flag = flag_dev;
+    job.done_seq = seq;
+    job.units = static_cast<uint32_t>(a.sz / 16);
+    job.r = a.r;
+    for (uint32_t i = 0; i < a.r; ++i)
+        for (uint32_t j = 0; j < a.k; ++j) {
+            const uint32_t* w = &kHostBank.w[uint32_t(a.coef[size_t(i) * a.coef_stride + j]) * 8];
+            std::memcpy(&job.tab[(i * a.k + j) * 5], w, 5 * sizeof(uint32_t));
+        }
+    static void (*const kOne[5])(const OneJob) = {nullptr, matapply_one<1>, matapply_one<2>, matapply_one<3>,
+                                                  matapply_one<4>};
+    hipLaunchKernelGGL(kOne[a.k], dim3(1), dim3(kBlock), 0, stream, job);
+    t_last_kernel = kOneNames[a.k];
+    return hipGetLastError();
 }
 
 hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream) {

@@ -78,6 +78,13 @@ bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes);
 void matapply_request_signal(uint32_t* flag_dev, uint32_t seq);
 bool matapply_signal_used();
 
+// The synchronous small call's launch (fec_abi.cpp run_single, every block in
+// the thread's pinned bounce buffer): k <= 4, r <= 8, one stripe of sz bytes,
+// sz a multiple of 16 and at most 4096 (whole 16-byte units, one workgroup).
+// matapply_one publishes `seq` at flag_dev (pinned host memory, may be null)
+// when it has finished.  hipErrorInvalidValue for other shapes.
+hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq);
+
 // Name of the table-kernel variant launch_apply uses for (k, r) when no
 // run-time specialised kernel applies (for tests / profiling).
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
