@@ -412,8 +412,9 @@ struct alignas(16) OneJob {
     uint8_t* out[8];
     uint32_t* done_flag;
     uint32_t units, r, done_seq, pad_;
-    uint32_t tab[4 * 8 * 5];  // row-major (r, j) coefficient tables, K per row
+    alignas(16) uint32_t tab[4 * 8 * 5];  // row-major (r, j) coefficient tables, K per row (16-byte loads)
 };
+static_assert(offsetof(OneJob, tab) % 16 == 0, "matapply_one loads the tables 16 bytes at a time");
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void matapply_one(const OneJob job) {
