@@ -1216,3 +1216,42 @@ def test_small_call_compact_kernel():
                 nums = list(range(m - k, m))
                 rec = dec.decode([out[i] for i in nums], nums)
                 assert b"".join(rec) == data.tobytes(), (k, m, sz)
+
+
+def test_batch_call_and_ctypes_paths_agree():
+    """capi's batched calls go through the extension (_fec.batch_call); the
+    ctypes binding of the same C-ABI functions must give the same bytes, the
+    same kernel and, for a bad call, the same status (a K=3/M=10 batch with
+    row padding and a K=20/M=60 batch, encode and decode)."""
+    import torch
+
+    capi.lib()
+    fast = capi._batch_call
+    assert fast is not None
+    for k, m, sz, ns in [(3, 10, 4093, 7), (20, 60, 52429, 3)]:
+        r, ld = m - k, (sz + 255) // 256 * 256
+        code = capi.Code(k, m)
+        data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda")
+        outs, recs, names = [], [], []
+        for use_fast in (True, False):
+            capi._batch_call = fast if use_fast else None
+            try:
+                par = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+                code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns,
+                                  flags=capi.FEC_FLAG_ROW_PADDING)
+                names.append(capi.last_kernel_name())
+                slots = list(range(m - k, m))
+                recv = par[:, r - k:].contiguous() if r >= k else None
+                rec = torch.zeros((ns, k, ld), dtype=torch.uint8, device="cuda")
+                code.decode_batch(recv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, k * ld, slots, sz, ns)
+                torch.cuda.synchronize()
+                outs.append(par[:, :, :sz].cpu())
+                recs.append(rec[:, :, :sz].cpu())
+                with pytest.raises(capi.FecError, match="out of range"):
+                    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, [m], sz, ns)
+            finally:
+                capi._batch_call = fast
+        assert names[0] == names[1], names
+        assert torch.equal(outs[0], outs[1]) and torch.equal(recs[0], recs[1]), (k, m)
+        assert torch.equal(recs[0], data[:, :, :sz].cpu()), (k, m)
+        assert (outs[0][0].numpy() == oracle.encode(k, m, data[0, :, :sz].cpu().numpy())).all(), (k, m)

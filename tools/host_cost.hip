@@ -98,6 +98,10 @@ int main() {
             printf("  hipGetFuncBySymbol failed\n");
         }
         void* args[] = {&a560};
+        printf("  hipLaunchKernel 560 B      %6.2f\n", per_call_us([&] {
+                   (void)hipLaunchKernel(reinterpret_cast<const void*>(empty_kernel<560>), dim3(1), dim3(256), args, 0,
+                                         st);
+               }));
         printf("  hipExtLaunchKernel 560 B   %6.2f\n", per_call_us([&] {
                    (void)hipExtLaunchKernel(reinterpret_cast<const void*>(empty_kernel<560>), dim3(1), dim3(256),
                                             args, 0, st, nullptr, nullptr, 0);

@@ -193,11 +193,16 @@ int pointer_device(const void* p, bool* pinned = nullptr, void** dev_ptr = nullp
 }
 
 int gpu_available() {
+    // the device count of a process does not change: cached once positive
+    static std::atomic<int> cached{0};
+    const int c = cached.load(std::memory_order_relaxed);
+    if (c > 0) return c;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) {
         (void)hipGetLastError();
         return 0;
     }
+    if (n > 0) cached.store(n, std::memory_order_relaxed);
     return n;
 }
 
@@ -246,12 +251,16 @@ hipError_t wait_signal(DevCtx& d, hipStream_t st) {
 // RAII: restore the caller's current device.
 struct DeviceGuard {
     int prev = -1;
+    bool changed = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
+        if (prev != dev) {
+            (void)hipSetDevice(dev);
+            changed = true;
+        }
     }
     ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
+        if (changed && prev >= 0) (void)hipSetDevice(prev);
     }
 };
 

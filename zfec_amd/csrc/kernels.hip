@@ -1161,6 +1161,17 @@ __global__ __launch_bounds__(kBlock) void matapply_small(const MatJob job) {
     }
 }
 
+// Launch through hipLaunchKernel itself: hipLaunchKernelGGL (<<<>>>) adds
+// __hipPushCallConfiguration / __hipPopCallConfiguration around it, and the
+// hipGetLastError after it is one more runtime call; together 0.2-0.35 us of
+// host time per launch (tools/host_cost.hip: "launch, 560 B kernarg" against
+// "hipLaunchKernel 560 B").  The returned status is the launch's.
+template <class J>
+hipError_t launch_job(const void* fn, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream, const J& job) {
+    void* args[] = {const_cast<J*>(&job)};
+    return hipLaunchKernel(fn, dim3(grid), dim3(block), args, lds, stream);
+}
+
 // Launches whose unit kernels would run fewer lanes than Config::small_lanes
 // (2048 by default) take matapply_small.
 hipError_t launch_small(MatJob& job, hipStream_t stream) {
@@ -1174,8 +1185,7 @@ hipError_t launch_small(MatJob& job, hipStream_t stream) {
     job.gs_c = static_cast<uint32_t>(wpr);
     job.gs_s = ub;
     const uint32_t grid = static_cast<uint32_t>((waves + kBlock / 64 - 1) / (kBlock / 64));
-    hipLaunchKernelGGL(matapply_small, dim3(grid), dim3(kBlock), 0, stream, job);
-    return hipGetLastError();
+    return launch_job(reinterpret_cast<const void*>(matapply_small), grid, kBlock, 0, stream, job);
 }
 
 // ---------------------------------------------------------------------------
@@ -1201,6 +1211,7 @@ void init_dispatch() {
 }
 
 thread_local const char* t_last_kernel = "";
+
 thread_local uint32_t* t_signal_flag = nullptr;
 thread_local uint32_t t_signal_seq = 0;
 thread_local bool t_signal_used = false;
@@ -1305,8 +1316,7 @@ hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
             t_signal_used = true;
         }
     }
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, stream, job);
-    return hipGetLastError();
+    return launch_job(reinterpret_cast<const void*>(fn), grid, kBlock, 0, stream, job);
 }
 
 typedef hipError_t (*RegLaunch)(const ApplySpec&, hipStream_t, uint32_t*);
@@ -1334,9 +1344,8 @@ hipError_t launch_pair(const ApplySpec& a, const ApplySpec& b, hipStream_t strea
     const StorePolicy sp = config().store;
     const bool sc1 = sp == kStoreNtSc1 || (sp == kStoreAuto && a.nstripes == 1 && b.nstripes == 1);
     void (*fn)(const PairJob<K, RA, RB>) = sc1 ? matapply_pair<K, RA, RB, 3> : matapply_pair<K, RA, RB, 0>;
-    hipLaunchKernelGGL(fn, dim3(ga + gb), dim3(kBlock), 0, stream, job);
     t_last_kernel = g_pair_names[K][RA][RB];
-    return hipGetLastError();
+    return launch_job(reinterpret_cast<const void*>(fn), ga + gb, kBlock, 0, stream, job);
 }
 
 typedef hipError_t (*PairLaunch)(const ApplySpec&, const ApplySpec&, hipStream_t);
@@ -1437,9 +1446,8 @@ hipError_t launch_lds(const ApplySpec& a, hipStream_t stream) {
     const uint64_t gstride = uint64_t(grid) * kBlock;
     job.gs_s = static_cast<uint32_t>(gstride / cps);
     job.gs_c = static_cast<uint32_t>(gstride % cps);
-    hipLaunchKernelGGL(v.fn, dim3(grid), dim3(kBlock), lds, stream, job);
     t_last_kernel = v.name;
-    return hipGetLastError();
+    return launch_job(reinterpret_cast<const void*>(v.fn), grid, kBlock, lds, stream, job);
 }
 
 // ---- matapply_bsg dispatch ------------------------------------------------------
@@ -1594,10 +1602,8 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
         job.cps = static_cast<uint32_t>(cps);
         job.gs_s = gs_s;
         job.gs_c = gs_c;
-        hipLaunchKernelGGL(reinterpret_cast<void (*)(const MatJob)>(const_cast<void*>(v.fn_karg)), dim3(grid),
-                           dim3(256), lds, stream, job);
         t_last_kernel = v.name;
-        return hipGetLastError();
+        return launch_job(v.fn_karg, grid, 256, lds, stream, job);
     }
     // pointers and coefficients in a device-side table
     const size_t bytes = 8 * size_t(k + r) + walk;
@@ -1625,9 +1631,7 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     job.ngroups = ngroups;
     job.pad_ = 0;
     job.table = d;
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(const BsgTblJob)>(const_cast<void*>(v.fn_tbl)), dim3(grid),
-                       dim3(256), lds, stream, job);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_job(v.fn_tbl, grid, 256, lds, stream, job)) != hipSuccess) return e;
     if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
     ring->busy[slot] = true;
     t_last_kernel = v.name_tbl;
@@ -1738,9 +1742,8 @@ hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev
         }
     static void (*const kOne[5])(const OneJob) = {nullptr, matapply_one<1>, matapply_one<2>, matapply_one<3>,
                                                   matapply_one<4>};
-    hipLaunchKernelGGL(kOne[a.k], dim3(1), dim3(kBlock), 0, stream, job);
     t_last_kernel = kOneNames[a.k];
-    return hipGetLastError();
+    return launch_job(reinterpret_cast<const void*>(kOne[a.k]), 1, kBlock, 0, stream, job);
 }
 
 hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream) {
