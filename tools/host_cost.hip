@@ -50,6 +50,10 @@ int main() {
     int dev = 0, cnt = 0;
     Arg<16> a16{};
     Arg<64> a64{};
+    Arg<72> a72{};
+    Arg<80> a80{};
+    Arg<96> a96{};
+    Arg<112> a112{};
     Arg<128> a128{};
     Arg<192> a192{};
     Arg<256> a256{};
@@ -57,7 +61,12 @@ int main() {
     Arg<560> a560{};
     Arg<1024> a1024{};
     Arg<2240> a2240{};
-    printf("host cost per call (us), %s\n", fec_version());
+    // the launch rate climbs over the first ~10^5 launches of a process (CPU
+    // clock, runtime pools): without this warm-up the first rows read up to
+    // 1 us slower than the same launches later in the run
+    for (int i = 0; i < 100000; ++i) hipLaunchKernelGGL(empty_kernel<16>, dim3(1), dim3(256), 0, st, a16);
+    (void)hipDeviceSynchronize();
+    printf("host cost per call (us), %s (after 10^5 warm-up launches)\n", fec_version());
     printf("  hipGetDeviceCount          %6.2f\n", per_call_us([&] { (void)hipGetDeviceCount(&cnt); }));
     printf("  hipGetDevice               %6.2f\n", per_call_us([&] { (void)hipGetDevice(&dev); }));
     printf("  hipPointerGetAttributes    %6.2f\n", per_call_us([&] { (void)hipPointerGetAttributes(&attr, src); }));
@@ -66,6 +75,14 @@ int main() {
            per_call_us([&] { hipLaunchKernelGGL(empty_kernel<16>, dim3(1), dim3(256), 0, st, a16); }));
     printf("  launch, 64 B kernarg       %6.2f\n",
            per_call_us([&] { hipLaunchKernelGGL(empty_kernel<64>, dim3(1), dim3(256), 0, st, a64); }));
+    printf("  launch, 72 B kernarg       %6.2f\n",
+           per_call_us([&] { hipLaunchKernelGGL(empty_kernel<72>, dim3(1), dim3(256), 0, st, a72); }));
+    printf("  launch, 80 B kernarg       %6.2f\n",
+           per_call_us([&] { hipLaunchKernelGGL(empty_kernel<80>, dim3(1), dim3(256), 0, st, a80); }));
+    printf("  launch, 96 B kernarg       %6.2f\n",
+           per_call_us([&] { hipLaunchKernelGGL(empty_kernel<96>, dim3(1), dim3(256), 0, st, a96); }));
+    printf("  launch, 112 B kernarg      %6.2f\n",
+           per_call_us([&] { hipLaunchKernelGGL(empty_kernel<112>, dim3(1), dim3(256), 0, st, a112); }));
     printf("  launch, 128 B kernarg      %6.2f\n",
            per_call_us([&] { hipLaunchKernelGGL(empty_kernel<128>, dim3(1), dim3(256), 0, st, a128); }));
     printf("  launch, 192 B kernarg      %6.2f\n",
