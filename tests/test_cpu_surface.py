@@ -307,6 +307,8 @@ def test_batch_call_matches_ctypes_binding():
         _fec.batch_call(0, code.ptr, -1, 1, 1, 1, 1, 1, [3], 1, 1, 0, 0)
     with pytest.raises(TypeError):
         _fec.batch_call(0, code.ptr, 1, 1, 1, 1, 1, 1, 3, 1, 1, 0, 0)
+    with pytest.raises(ValueError, match="kind"):
+        _fec.batch_call(2, code.ptr, 1, 1, 1, 1, 1, 1, [3], 1, 1, 0, 0)
 
 
 def test_batch_jobs_validation():

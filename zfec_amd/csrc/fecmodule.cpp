@@ -664,6 +664,10 @@ PyObject* py_batch_call(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
         v[i] = PyLong_AsSize_t(args[i]);
         if (v[i] == size_t(-1) && PyErr_Occurred()) return nullptr;
     }
+    if (v[0] > 1) {
+        PyErr_Format(PyExc_ValueError, "batch_call: kind must be 0 (encode) or 1 (decode), not %zu", v[0]);
+        return nullptr;
+    }
     PyObject* seq = PySequence_Fast(args[8], "batch_call: nums must be a tuple or list");
     if (!seq) return nullptr;
     const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
