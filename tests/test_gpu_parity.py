@@ -1196,12 +1196,17 @@ def test_small_call_signal_under_load():
     assert not errors, errors
 
 
-def test_small_call_compact_kernel():
+@pytest.mark.parametrize("inline", [True, False])
+def test_small_call_compact_kernel(inline, knobs):
     """Synchronous calls from bytes with k <= 4, r <= 8 and blocks of at most
     4 KiB run on the compact one-workgroup kernel (kernels.hip matapply_one,
-    whole 16-byte units in the bounce buffer): bit-exact against the oracle
-    for every such (k, r) at sizes around the unit and the 4 KiB limit; one
-    byte past the limit takes the general kernels."""
+    whole 16-byte units in the bounce buffer; inputs inside the argument
+    block where k x sz fits 4,352 bytes, or read from the bounce buffer with
+    ZFEC_HIP_SMALL_INLINE=0): bit-exact against the oracle for every such
+    (k, r) at sizes around the unit and the 4 KiB limit; one byte past the
+    limit takes the general kernels."""
+    if not inline:
+        knobs(ZFEC_HIP_SMALL_INLINE="0")
     rng = np.random.default_rng(77)
     for k in range(1, 5):
         for m in range(k + 1, k + 9):
@@ -1210,7 +1215,9 @@ def test_small_call_compact_kernel():
                 data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
                 out = enc.encode([data[i].tobytes() for i in range(k)])
                 name = capi.last_kernel_name()
-                assert (name == "matapply_one<%d>" % k) == (sz <= 4096), (k, m, sz, name)
+                ksz = min((sz + 255) // 256 * 256, (sz + 127) // 128 * 128)
+                want = "matapply_one<%d,inline>" % k if inline and k * ksz <= 4352 else "matapply_one<%d>" % k
+                assert (name == want) == (sz <= 4096), (k, m, sz, name, want)
                 par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
                 assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
                 nums = list(range(m - k, m))

@@ -69,6 +69,7 @@ Config* read_env() {
     c->stage_chunk = sc >= (64u << 10) ? sc / 4096 * 4096 : 0;
     c->zc_wide = env_flag("ZFEC_HIP_ZC_WIDE", false);
     c->small_one = env_flag("ZFEC_HIP_SMALL_ONE", true);
+    c->small_inline = env_flag("ZFEC_HIP_SMALL_INLINE", true);
     c->trace_host = env("ZFEC_HIP_TRACE_HOST") != nullptr;
     const char* q = env("ZFEC_HIP_QUIET");
     c->quiet = q && q[0] == '1';

@@ -850,7 +850,19 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         }
         if (pooled) HostPool::get().wait(&latch);
     };
-    copy_blocks(true);
+    // Every block in the bounce buffer: its slots are 256-byte multiples, so
+    // the kernel may run each row out to its next 128-byte line (whole 16-byte
+    // units, no byte-wise tail: over PCIe each tail byte load is a round trip
+    // of its own); the bytes past sz are never copied out.
+    const size_t ksz = nhost == size_t(k) + r ? std::min(slot, align_up(sz, 128)) : sz;
+    // The compact one-workgroup kernel takes the inputs inside its argument
+    // block where they fit (kernels.hip OneJobInline): no copy into the bounce
+    // buffer, no PCIe reads in the kernel.
+    const bool one_shape = k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && cfg.small_one &&
+                           sz * nhost <= kZeroCopyLimit;
+    const bool inline_in = one_shape && cfg.small_inline && nin == k && nhost == size_t(k) + r &&
+                           size_t(k) * ksz <= kOneInlineBytes;
+    if (!inline_in) copy_blocks(true);
     // Zero-copy only for the register kernels (k <= 4, r <= 8), which issue
     // all their input loads at once: the wide-code kernels read inputs in
     // groups, each group a PCIe round trip of its own (K=20/M=60, 4 KiB stripe:
@@ -859,16 +871,11 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // them zero-copy (A/B runs).
     const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide;
     bool signalled = false;
-    // Every block in the bounce buffer: its slots are 256-byte multiples, so
-    // the kernel may run each row out to its next 128-byte line (whole 16-byte
-    // units, no byte-wise tail: over PCIe each tail byte load is a round trip
-    // of its own); the bytes past sz are never copied out.
-    const size_t ksz = nhost == size_t(k) + r ? std::min(slot, align_up(sz, 128)) : sz;
     if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = hbd + slot * (nin + q);
-        if (k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && cfg.small_one) {
+        if (one_shape) {
             // whole 16-byte units in one workgroup: the compact kernel
             // (kernels.hip matapply_one), which signals its own completion
             uint32_t* f = signal_slot(*d);
@@ -884,7 +891,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
             a.in_sstride = a.out_sstride = 0;
             a.accumulate = false;
             ++t_launches;
-            const hipError_t le = launch_one(a, st, f, f ? d->seq : 0);
+            const hipError_t le = launch_one(a, st, f, f ? d->seq : 0, inline_in ? in : nullptr, sz);
             if (le != hipSuccess) return hip_fail(le, "launch_one");
             signalled = f != nullptr;
         } else {

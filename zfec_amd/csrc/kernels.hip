@@ -416,8 +416,24 @@ struct alignas(16) OneJob {
 };
 static_assert(offsetof(OneJob, tab) % 16 == 0, "matapply_one loads the tables 16 bytes at a time");
 
-template <int K>
-__global__ __launch_bounds__(kBlock) void matapply_one(const OneJob job) {
+// INL: the k input blocks ride in the argument block itself (k x units x 16
+// bytes at most kOneInline), which HIP writes to device memory with the
+// launch: the kernel reads them there instead of across PCIe from the bounce
+// buffer, and the caller's bytes need no copy into pinned memory first
+// (tools/inline_probe.hip: 7.2 against 7.9 us launch to completion seen for
+// a 4 KiB K=3/M=10 encode stand-in).
+constexpr uint32_t kOneInline = kOneInlineBytes;  // a 4 KiB K=3 stripe: 3 x 88 units of 16 bytes = 4,224
+struct alignas(16) OneJobInline {
+    OneJob job;
+    u32x4 data[kOneInline / 16];  // input j's unit u at data[j * units + u]
+};
+
+__device__ __forceinline__ const OneJob& one_job(const OneJob& a) { return a; }
+__device__ __forceinline__ const OneJob& one_job(const OneJobInline& a) { return a.job; }
+
+template <int K, bool INL, class J>
+__global__ __launch_bounds__(kBlock) void matapply_one(const J arg) {
+    const OneJob& job = one_job(arg);
     // the coefficient tables (up to 160 dwords) reach LDS in ONE vector load
     // round trip (a lane per 16 bytes of the argument segment), not in a
     // chain of scalar loads per output row
@@ -430,8 +446,14 @@ __global__ __launch_bounds__(kBlock) void matapply_one(const OneJob job) {
     }
     u32x4 x[K];
     if (u < job.units) {
+        if constexpr (INL) {
+            const KPtr<OneJobInline> kj = kernarg_job<OneJobInline>();
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + size_t(u) * 16);
+            for (int j = 0; j < K; ++j) x[j] = kj->data[j * job.units + u];
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = load16(job.in[j] + size_t(u) * 16);
+        }
     }
     __syncthreads();
     if (u < job.units) {
@@ -1719,31 +1741,48 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     return launch_lds(a, stream);
 }
 
-hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq) {
-    static const char* const kOneNames[5] = {"", "matapply_one<1>", "matapply_one<2>", "matapply_one<3>",
-                                             "matapply_one<4>"};
+hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq,
+                      const uint8_t* const* host_in, uint64_t host_sz) {
+    static const char* const kOneNames[2][5] = {
+        {"", "matapply_one<1>", "matapply_one<2>", "matapply_one<3>", "matapply_one<4>"},
+        {"", "matapply_one<1,inline>", "matapply_one<2,inline>", "matapply_one<3,inline>", "matapply_one<4,inline>"}};
     if (a.k < 1 || a.k > 4 || a.r < 1 || a.r > 8 || a.nstripes != 1 || a.sz == 0 || a.sz % 16 || a.sz > 4096 ||
         a.accumulate || a.coef_stride < a.k)
         return hipErrorInvalidValue;
     t_signal_flag = nullptr;  // an unconsumed launch_apply request must not outlive this launch
     t_signal_used = false;
-    OneJob job;
+    const uint32_t units = static_cast<uint32_t>(a.sz / 16);
+    const bool inl = host_in && host_sz <= a.sz && uint64_t(a.k) * units * 16 <= kOneInline;
+    thread_local OneJobInline big;  // ~5 KiB: not on the stack of every call
+    OneJob& job = big.job;
     std::memset(&job, 0, sizeof job);
     for (uint32_t j = 0; j < a.k; ++j) job.in[j] = a.in[j];
     for (uint32_t i = 0; i < a.r; ++i) job.out[i] = a.out[i];
     job.done_flag = flag_dev;
     job.done_seq = seq;
-    job.units = static_cast<uint32_t>(a.sz / 16);
+    job.units = units;
     job.r = a.r;
     for (uint32_t i = 0; i < a.r; ++i)
         for (uint32_t j = 0; j < a.k; ++j) {
             const uint32_t* w = &kHostBank.w[uint32_t(a.coef[size_t(i) * a.coef_stride + j]) * 8];
             std::memcpy(&job.tab[(i * a.k + j) * 5], w, 5 * sizeof(uint32_t));
         }
-    static void (*const kOne[5])(const OneJob) = {nullptr, matapply_one<1>, matapply_one<2>, matapply_one<3>,
-                                                  matapply_one<4>};
-    t_last_kernel = kOneNames[a.k];
-    return launch_job(reinterpret_cast<const void*>(kOne[a.k]), 1, kBlock, 0, stream, job);
+    typedef void (*OneFn)(const OneJob);
+    typedef void (*OneInlFn)(const OneJobInline);
+    static const OneFn kOne[5] = {nullptr, matapply_one<1, false, OneJob>, matapply_one<2, false, OneJob>,
+                                  matapply_one<3, false, OneJob>, matapply_one<4, false, OneJob>};
+    static const OneInlFn kOneInl[5] = {nullptr, matapply_one<1, true, OneJobInline>,
+                                        matapply_one<2, true, OneJobInline>, matapply_one<3, true, OneJobInline>,
+                                        matapply_one<4, true, OneJobInline>};
+    t_last_kernel = kOneNames[inl ? 1 : 0][a.k];
+    if (!inl) return launch_job(reinterpret_cast<const void*>(kOne[a.k]), 1, kBlock, 0, stream, job);
+    // the caller's host blocks, each padded with zeros to its whole units
+    uint8_t* d = reinterpret_cast<uint8_t*>(big.data);
+    for (uint32_t j = 0; j < a.k; ++j) {
+        std::memcpy(d + size_t(j) * units * 16, host_in[j], host_sz);
+        std::memset(d + size_t(j) * units * 16 + host_sz, 0, size_t(units) * 16 - host_sz);
+    }
+    return launch_job(reinterpret_cast<const void*>(kOneInl[a.k]), 1, kBlock, 0, stream, big);
 }
 
 hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream) {

@@ -82,8 +82,13 @@ bool matapply_signal_used();
 // the thread's pinned bounce buffer): k <= 4, r <= 8, one stripe of sz bytes,
 // sz a multiple of 16 and at most 4096 (whole 16-byte units, one workgroup).
 // matapply_one publishes `seq` at flag_dev (pinned host memory, may be null)
-// when it has finished.  hipErrorInvalidValue for other shapes.
-hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq);
+// when it has finished.  host_in (may be null): the k input blocks of host_sz
+// bytes each in host memory; where they fit (k x sz rounded to 16 bytes at
+// most 4,352 bytes) they are copied into the kernel's argument block and
+// a.in is not read.  hipErrorInvalidValue for other shapes.
+constexpr uint32_t kOneInlineBytes = 4352;  // inline input capacity of matapply_one's argument block
+hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq,
+                      const uint8_t* const* host_in = nullptr, uint64_t host_sz = 0);
 
 // Name of the table-kernel variant launch_apply uses for (k, r) when no
 // run-time specialised kernel applies (for tests / profiling).
