@@ -1262,3 +1262,29 @@ def test_batch_call_and_ctypes_paths_agree():
         assert torch.equal(outs[0], outs[1]) and torch.equal(recs[0], recs[1]), (k, m)
         assert torch.equal(recs[0], data[:, :, :sz].cpu()), (k, m)
         assert (outs[0][0].numpy() == oracle.encode(k, m, data[0, :, :sz].cpu().numpy())).all(), (k, m)
+
+
+@pytest.mark.parametrize("mode", ["signal", "sync"])
+def test_medium_call_wait_modes(mode, knobs):
+    """Synchronous calls from bytes too large for one workgroup: on the
+    zero-copy path (at most 256 KiB of host blocks, k <= 4) the stream writes
+    the call's sequence number into the pinned completion word after the
+    kernel (hipStreamWriteValue32) and the caller spins on it; the copy path
+    and ZFEC_HIP_WAIT=sync wait in hipStreamSynchronize.  Bit-exact against
+    the oracle either way."""
+    if mode == "sync":
+        knobs(ZFEC_HIP_WAIT="sync")
+    rng = np.random.default_rng(65536)
+    for k, m in ((3, 10), (10, 16)):
+        enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+        for stripe in (20000, 65536, 131072, 180000):  # all below the staged path (run_staged)
+            sz = -(-stripe // k)
+            data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+            out = enc.encode([data[i].tobytes() for i in range(k)])
+            zero_copy = k <= 4 and (sz * m) <= (1 << 20)
+            assert capi.last_wait() == (1 if mode == "signal" and zero_copy else 0), (mode, k, stripe)
+            par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+            assert (par == oracle.encode(k, m, data)).all(), (k, m, stripe)
+            nums = list(range(m - k, m))
+            rec = dec.decode([out[i] for i in nums], nums)
+            assert b"".join(rec) == data.tobytes(), (k, m, stripe)

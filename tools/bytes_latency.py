@@ -30,10 +30,10 @@ def main():
     rng = np.random.default_rng(0)
     res = []
     for k, m in [(3, 10), (20, 60)]:
-        for stripe in [4096, 65536, 1 << 20, 4 << 20]:
+        for stripe in [4096, 65536, 131072, 1 << 20, 4 << 20]:  # 128 KiB: a tahoe-lafs segment
             sz = -(-stripe // k)
             blocks = [rng.integers(0, 256, sz, dtype=np.uint8).tobytes() for _ in range(k)]
-            n = 2000 if stripe <= 65536 else (200 if stripe <= 1 << 20 else 50)
+            n = 2000 if stripe <= 131072 else (200 if stripe <= 1 << 20 else 50)
             row = {"k": k, "m": m, "stripe": stripe}
             impls = [("gpu", zfec_amd)] + ([("cpu_ref", ref)] if ref is not None else [])
             for name, mod in impls:

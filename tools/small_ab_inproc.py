@@ -5,7 +5,11 @@ between ZFEC_HIP_* settings re-read with fec_reload_config, so the drift of
 the host's launch rate within a process hits every variant alike.  Medians of
 the per-block means over the rounds (us per call).
 
-    python tools/small_ab_inproc.py [--rounds 12] [--n 2000]
+    python tools/small_ab_inproc.py [--rounds 12] [--n 2000] [--set kernel|wait] [--stripe 4096]
+
+--set kernel: the small-call kernels (inline / bounce buffer / matapply_reg);
+--set wait:   the completion wait (completion word / hipStreamSynchronize);
+--set zc:     how far the kernel reads and writes the bounce buffer in place.
 """
 import argparse
 import json
@@ -19,16 +23,22 @@ import numpy as np  # noqa: E402
 import zfec_amd  # noqa: E402
 from zfec_amd import capi  # noqa: E402
 
-VARIANTS = {"inline": {}, "pinned": {"ZFEC_HIP_SMALL_INLINE": "0"}, "reg": {"ZFEC_HIP_SMALL_ONE": "0"}}
+SETS = {"kernel": {"inline": {}, "pinned": {"ZFEC_HIP_SMALL_INLINE": "0"}, "reg": {"ZFEC_HIP_SMALL_ONE": "0"}},
+        "wait": {"signal": {}, "sync": {"ZFEC_HIP_WAIT": "sync"}},
+        "zc": {"zc256k": {}, "zc1m": {"ZFEC_HIP_ZC_LIMIT": str(1 << 20)}, "zc4m": {"ZFEC_HIP_ZC_LIMIT": str(4 << 20)}}}
+KNOBS = ("ZFEC_HIP_SMALL_INLINE", "ZFEC_HIP_SMALL_ONE", "ZFEC_HIP_WAIT", "ZFEC_HIP_ZC_LIMIT")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--n", type=int, default=2000)
+    ap.add_argument("--set", default="kernel", choices=sorted(SETS))
+    ap.add_argument("--stripe", type=int, default=4096)
     a = ap.parse_args()
+    VARIANTS = SETS[a.set]
     k, m = 3, 10
-    sz = -(-4096 // k)
+    sz = -(-a.stripe // k)
     blocks = [np.random.default_rng(i).integers(0, 256, sz, dtype=np.uint8).tobytes() for i in range(k)]
     enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
     out = enc.encode(blocks)
@@ -36,7 +46,7 @@ def main():
     sec = [out[i] for i in nums]
 
     def setv(env):
-        for key in ("ZFEC_HIP_SMALL_INLINE", "ZFEC_HIP_SMALL_ONE"):
+        for key in KNOBS:
             os.environ.pop(key, None)
         os.environ.update(env)
         capi.reload_config()
@@ -63,7 +73,8 @@ def main():
     summary = {v: {"kernel": d["kernel"], "encode_us_median": round(float(np.median(d["enc"])), 2),
                    "decode_us_median": round(float(np.median(d["dec"])), 2),
                    "encode_us_min": round(float(np.min(d["enc"])), 2)} for v, d in res.items()}
-    print(json.dumps({"rounds": a.rounds, "calls_per_block": a.n, "variants": summary}, indent=1))
+    print(json.dumps({"k": k, "m": m, "stripe": a.stripe, "rounds": a.rounds, "calls_per_block": a.n,
+                      "variants": summary}, indent=1))
 
 
 if __name__ == "__main__":

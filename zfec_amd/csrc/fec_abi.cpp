@@ -412,8 +412,12 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
 // not for many small blocks (K=20/M=60, 256 KiB stripe of 13 KB blocks: 260
 // vs 122 us; tools/host_lat_ab.py, profiles/r02_host_lat_ab.log).
 constexpr size_t kStageMinBlock = size_t(64) << 10;
-// Up to this many bytes the kernel accesses the bounce buffer in place.
-constexpr size_t kZeroCopyLimit = size_t(256) << 10;
+// Up to Config::zc_limit bytes (1 MiB: every small call of k <= 4, r <= 8,
+// since larger ones take the staged path) the kernel accesses the bounce
+// buffer in place.  Round 2 stopped at 256 KiB; an interleaved A/B of 100-150
+// KB K=3/M=10 stripes from bytes (tools/small_ab_inproc.py --set zc,
+// profiles/r03_zc_ab.log): encode 44.5-51.3 -> 25.1-33.0 us, decode
+// 17.0-38.3 -> 16.9-19.8 us against one H2D and one D2H copy.
 // Small calls: from Config::pool_copy_min bytes per direction the
 // bounce-buffer copies run on the host pool.  Off by default: waking the pool
 // costs more than it saves below 4 MiB (1 MiB K=3/M=10 stripe: 255 us pooled
@@ -822,11 +826,11 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         return run_staged(*d, coef, k, r, in, out, sz, m, st);
 
     // small call: pack the host inputs into the thread's pinned buffer.  Up to
-    // kZeroCopyLimit bytes the kernel reads them and writes the host outputs
+    // Config::zc_limit bytes the kernel reads them and writes the host outputs
     // there in place over PCIe (no copy calls: 4 KiB K=3/M=10 encode 21.9 ->
-    // 16.6 us per call); above it one H2D and one D2H DMA of the packed blocks
-    // move them faster than the kernel's own PCIe accesses (1 MiB: 168 vs
-    // 186 us).  Device-resident blocks are used in place.  Then unpack.
+    // 16.6 us per call, 128 KiB 46.8 -> 26.6 us); wide codes (and calls past
+    // the limit) move the packed blocks with one H2D and one D2H copy.
+    // Device-resident blocks are used in place.  Then unpack.
     m.din.assign(in, in + k);
     m.dout.assign(out, out + r);
     const size_t slot = align_up(sz, 256);
@@ -859,7 +863,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // block where they fit (kernels.hip OneJobInline): no copy into the bounce
     // buffer, no PCIe reads in the kernel.
     const bool one_shape = k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && cfg.small_one &&
-                           sz * nhost <= kZeroCopyLimit;
+                           sz * nhost <= cfg.zc_limit;
     const bool inline_in = one_shape && cfg.small_inline && nin == k && nhost == size_t(k) + r &&
                            size_t(k) * ksz <= kOneInlineBytes;
     if (!inline_in) copy_blocks(true);
@@ -871,7 +875,8 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // them zero-copy (A/B runs).
     const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide;
     bool signalled = false;
-    if (sz * nhost <= kZeroCopyLimit && zc_kernel) {
+    const bool zero_copy = sz * nhost <= cfg.zc_limit && zc_kernel;
+    if (zero_copy) {
         uint8_t* hbd = static_cast<uint8_t*>(d->hbuf_dev);
         for (size_t q = 0; q < nin; ++q) m.din[m.in_host[q]] = hbd + slot * q;
         for (size_t q = 0; q < nout; ++q) m.dout[m.out_host[q]] = hbd + slot * (nin + q);
@@ -917,6 +922,20 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
         if (nout && (e = hipMemcpyAsync(hb + slot * nin, base + slot * nin, slot * nout, hipMemcpyDeviceToHost,
                                         st)) != hipSuccess)
             return hip_fail(e, "hipMemcpyAsync D2H");
+    }
+    if (!signalled && zero_copy) {
+        // a zero-copy launch of several workgroups: the stream itself writes
+        // the call's sequence number into the pinned completion word after the
+        // kernel, and the thread spins on that (64 KiB K=3/M=10 encode 23.8 ->
+        // 21.2 us, decode 19.1 -> 16.4 us in an interleaved A/B,
+        // profiles/r03_wait_ab.log).  Not behind the copy path's D2H copy:
+        // there it measured 6-7 us slower than hipStreamSynchronize.
+        if (uint32_t* f = signal_slot(*d)) {
+            if (hipStreamWriteValue32(st, f, d->seq, 0) == hipSuccess)
+                signalled = true;
+            else
+                (void)hipGetLastError();
+        }
     }
     t_last_wait = signalled ? 1 : 0;
     if ((e = signalled ? wait_signal(*d, st) : hipStreamSynchronize(st)) != hipSuccess)
