@@ -9,7 +9,9 @@ the per-block means over the rounds (us per call).
 
 --set kernel: the small-call kernels (inline / bounce buffer / matapply_reg);
 --set wait:   the completion wait (completion word / hipStreamSynchronize);
---set zc:     how far the kernel reads and writes the bounce buffer in place.
+--set zc:     how far the kernel reads and writes the bounce buffer in place;
+--set stage:  larger calls staged through the host pool, or packed into the
+              bounce buffer (kernel in place / with copies).
 """
 import argparse
 import json
@@ -25,8 +27,15 @@ from zfec_amd import capi  # noqa: E402
 
 SETS = {"kernel": {"inline": {}, "pinned": {"ZFEC_HIP_SMALL_INLINE": "0"}, "reg": {"ZFEC_HIP_SMALL_ONE": "0"}},
         "wait": {"signal": {}, "sync": {"ZFEC_HIP_WAIT": "sync"}},
-        "zc": {"zc256k": {}, "zc1m": {"ZFEC_HIP_ZC_LIMIT": str(1 << 20)}, "zc4m": {"ZFEC_HIP_ZC_LIMIT": str(4 << 20)}}}
-KNOBS = ("ZFEC_HIP_SMALL_INLINE", "ZFEC_HIP_SMALL_ONE", "ZFEC_HIP_WAIT", "ZFEC_HIP_ZC_LIMIT")
+        "zc": {"zc256k": {"ZFEC_HIP_ZC_LIMIT": str(256 << 10)}, "zc1m": {"ZFEC_HIP_ZC_LIMIT": str(1 << 20)},
+               "zc2m": {}},
+        "stage": {"default": {},
+                  "staged": {"ZFEC_HIP_ZC_LIMIT": str(256 << 10)},
+                  "bounce_inplace": {"ZFEC_HIP_STAGE_MIN": str(64 << 20), "ZFEC_HIP_PACK_LIMIT": str(64 << 20),
+                                     "ZFEC_HIP_ZC_LIMIT": str(64 << 20)},
+                  "bounce_copies": {"ZFEC_HIP_STAGE_MIN": str(64 << 20), "ZFEC_HIP_PACK_LIMIT": str(64 << 20)}}}
+KNOBS = ("ZFEC_HIP_SMALL_INLINE", "ZFEC_HIP_SMALL_ONE", "ZFEC_HIP_WAIT", "ZFEC_HIP_ZC_LIMIT", "ZFEC_HIP_STAGE_MIN",
+         "ZFEC_HIP_PACK_LIMIT")
 
 
 def main():

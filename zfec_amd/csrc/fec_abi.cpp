@@ -412,8 +412,8 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
 // not for many small blocks (K=20/M=60, 256 KiB stripe of 13 KB blocks: 260
 // vs 122 us; tools/host_lat_ab.py, profiles/r02_host_lat_ab.log).
 constexpr size_t kStageMinBlock = size_t(64) << 10;
-// Up to Config::zc_limit bytes (1 MiB: every small call of k <= 4, r <= 8,
-// since larger ones take the staged path) the kernel accesses the bounce
+// Up to Config::zc_limit bytes (1.5 MiB; calls of k <= 4, r <= 8 up to that
+// size stay on the bounce buffer, run_single) the kernel accesses the bounce
 // buffer in place.  Round 2 stopped at 256 KiB; an interleaved A/B of 100-150
 // KB K=3/M=10 stripes from bytes (tools/small_ab_inproc.py --set zc,
 // profiles/r03_zc_ab.log): encode 44.5-51.3 -> 25.1-33.0 us, decode
@@ -821,8 +821,17 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
             return hip_fail(e, "hipStreamSynchronize");
         return set_status(FEC_OK);
     }
-    // large pageable blocks: staged through pinned slots by the host threads
-    if (sz * nhost > cfg.pack_limit || (sz * nhost > cfg.stage_min && sz >= kStageMinBlock))
+    // large pageable blocks: staged through pinned slots by the host threads.
+    // Calls whose kernel can use the bounce buffer in place (k <= 4, r <= 8)
+    // stay on it up to Config::zc_limit: K=3/M=10 from bytes, 256 KiB stripes
+    // (874 KB of host blocks) encode in 47-57 us there against 62-71 us staged
+    // and decode in 30-35 against 45-52; 512 KiB stripes (1.75 MB) encode
+    // 78-97 against 84-86 us (box-dependent: staged from 1.5 MiB) and decode
+    // (1.05 MB) 49-56 against 61 us; 1 MiB stripes 186 against 159 us
+    // (tools/small_ab_inproc.py --set stage, profiles/r03_stage_ab.log).
+    const bool zc_shape = (k <= 4 && r <= 8) || cfg.zc_wide;
+    const size_t stage_from = zc_shape ? std::max(cfg.stage_min, cfg.zc_limit) : cfg.stage_min;
+    if (sz * nhost > cfg.pack_limit || (sz * nhost > stage_from && sz >= kStageMinBlock))
         return run_staged(*d, coef, k, r, in, out, sz, m, st);
 
     // small call: pack the host inputs into the thread's pinned buffer.  Up to
