@@ -1288,3 +1288,24 @@ def test_medium_call_wait_modes(mode, knobs):
             nums = list(range(m - k, m))
             rec = dec.decode([out[i] for i in nums], nums)
             assert b"".join(rec) == data.tobytes(), (k, m, stripe)
+
+
+@pytest.mark.parametrize("in_place", [True, False])
+def test_wide_small_calls_bounce_modes(in_place, knobs):
+    """Small calls of wide codes from bytes: with ZFEC_HIP_ZC_WIDE_LIMIT=256 KiB
+    the kernel reads and writes the pinned bounce buffer in place over PCIe up
+    to that many host bytes; with 0 (the default) one H2D and one D2H copy
+    move them.  Bit-exact against the oracle in both modes, encode and decode."""
+    knobs(ZFEC_HIP_ZC_WIDE_LIMIT=str(256 << 10) if in_place else "0")
+    rng = np.random.default_rng(2060)
+    for k, m in ((20, 60), (10, 16), (5, 9), (3, 12)):
+        enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
+        for stripe in (1, 4096, 20000, 65536):
+            sz = -(-stripe // k)
+            data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+            out = enc.encode([data[i].tobytes() for i in range(k)])
+            par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
+            assert (par == oracle.encode(k, m, data)).all(), (k, m, stripe, in_place)
+            nums = list(range(m - k, m))
+            rec = dec.decode([out[i] for i in nums], nums)
+            assert b"".join(rec) == data.tobytes(), (k, m, stripe, in_place)

@@ -11,7 +11,9 @@ the per-block means over the rounds (us per call).
 --set wait:   the completion wait (completion word / hipStreamSynchronize);
 --set zc:     how far the kernel reads and writes the bounce buffer in place;
 --set stage:  larger calls staged through the host pool, or packed into the
-              bounce buffer (kernel in place / with copies).
+              bounce buffer (kernel in place / with copies);
+--set pool:   the bounce buffer's copies on the calling thread or on the host pool;
+--set zcwide: wide codes (k > 4 or r > 8) with the bounce buffer's copies or in place.
 """
 import argparse
 import json
@@ -33,9 +35,14 @@ SETS = {"kernel": {"inline": {}, "pinned": {"ZFEC_HIP_SMALL_INLINE": "0"}, "reg"
                   "staged": {"ZFEC_HIP_ZC_LIMIT": str(256 << 10)},
                   "bounce_inplace": {"ZFEC_HIP_STAGE_MIN": str(64 << 20), "ZFEC_HIP_PACK_LIMIT": str(64 << 20),
                                      "ZFEC_HIP_ZC_LIMIT": str(64 << 20)},
-                  "bounce_copies": {"ZFEC_HIP_STAGE_MIN": str(64 << 20), "ZFEC_HIP_PACK_LIMIT": str(64 << 20)}}}
+                  "bounce_copies": {"ZFEC_HIP_STAGE_MIN": str(64 << 20), "ZFEC_HIP_PACK_LIMIT": str(64 << 20)}},
+        "zcwide": {"copies": {}, "inplace256k": {"ZFEC_HIP_ZC_WIDE_LIMIT": str(256 << 10)},
+                   "inplace": {"ZFEC_HIP_ZC_WIDE": "1"}},
+        "pool": {"thread": {}, "pool64k": {"ZFEC_HIP_POOL_COPY_MIN": str(64 << 10)},
+                 "pool256k": {"ZFEC_HIP_POOL_COPY_MIN": str(256 << 10)}}}
 KNOBS = ("ZFEC_HIP_SMALL_INLINE", "ZFEC_HIP_SMALL_ONE", "ZFEC_HIP_WAIT", "ZFEC_HIP_ZC_LIMIT", "ZFEC_HIP_STAGE_MIN",
-         "ZFEC_HIP_PACK_LIMIT")
+         "ZFEC_HIP_PACK_LIMIT", "ZFEC_HIP_POOL_COPY_MIN", "ZFEC_HIP_ZC_WIDE",
+         "ZFEC_HIP_ZC_WIDE_LIMIT")
 
 
 def main():
@@ -44,9 +51,10 @@ def main():
     ap.add_argument("--n", type=int, default=2000)
     ap.add_argument("--set", default="kernel", choices=sorted(SETS))
     ap.add_argument("--stripe", type=int, default=4096)
+    ap.add_argument("--km", default="3,10", help="k,m")
     a = ap.parse_args()
     VARIANTS = SETS[a.set]
-    k, m = 3, 10
+    k, m = (int(x) for x in a.km.split(","))
     sz = -(-a.stripe // k)
     blocks = [np.random.default_rng(i).integers(0, 256, sz, dtype=np.uint8).tobytes() for i in range(k)]
     enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)

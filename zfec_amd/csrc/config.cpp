@@ -69,6 +69,7 @@ Config* read_env() {
     c->stage_chunk = sc >= (64u << 10) ? sc / 4096 * 4096 : 0;
     c->zc_wide = env_flag("ZFEC_HIP_ZC_WIDE", false);
     c->zc_limit = env_size("ZFEC_HIP_ZC_LIMIT", size_t(3) << 19);  // 1.5 MiB
+    c->zc_wide_limit = env_size("ZFEC_HIP_ZC_WIDE_LIMIT", 0);
     c->small_one = env_flag("ZFEC_HIP_SMALL_ONE", true);
     c->small_inline = env_flag("ZFEC_HIP_SMALL_INLINE", true);
     c->trace_host = env("ZFEC_HIP_TRACE_HOST") != nullptr;

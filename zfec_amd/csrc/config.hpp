@@ -33,6 +33,7 @@ struct Config {
     size_t pool_copy_min;  // ZFEC_HIP_POOL_COPY_MIN: bounce-buffer copies on the host pool from this size
     size_t stage_chunk;    // ZFEC_HIP_STAGE_CHUNK: bytes of each block per staged chunk (0: automatic)
     bool zc_wide;          // ZFEC_HIP_ZC_WIDE=1: wide codes read the bounce buffer in place too
+    size_t zc_wide_limit;  // ZFEC_HIP_ZC_WIDE_LIMIT: host bytes up to which wide codes' kernels use it in place (0: off)
     size_t zc_limit;       // ZFEC_HIP_ZC_LIMIT: host bytes up to which small calls' kernels use the bounce buffer in place (1.5 MiB)
     bool small_one;        // ZFEC_HIP_SMALL_ONE=0: small synchronous calls launch matapply_reg (A/B)
     bool small_inline;     // ZFEC_HIP_SMALL_INLINE=0: matapply_one reads its inputs from the bounce buffer (A/B)

@@ -882,7 +882,12 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // 40 us in the kernel over PCIe; tools/small_call_probe.py under
     // rocprofv3, profiles/r02_small_calls.log).  ZFEC_HIP_ZC_WIDE=1 keeps
     // them zero-copy (A/B runs).
-    const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide;
+    // Wide codes in place for small packs (Config::zc_wide_limit, off by
+    // default until a GPU run validates it): K=20/M=60 from bytes, 4 KiB
+    // stripes encode in 20.5 us in place against 25.3 us with the copies, 64 KiB
+    // 44.7 against 47.9 us, but 128 KiB (393 KB of host blocks) 63.8 against
+    // 57.9 us (tools/small_ab_inproc.py --set zcwide, profiles/r03_zcwide_ab.log).
+    const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide || sz * nhost <= cfg.zc_wide_limit;
     bool signalled = false;
     const bool zero_copy = sz * nhost <= cfg.zc_limit && zc_kernel;
     if (zero_copy) {
