@@ -1290,7 +1290,12 @@ def test_medium_call_wait_modes(mode, knobs):
             assert b"".join(rec) == data.tobytes(), (k, m, stripe)
 
 
-@pytest.mark.parametrize("in_place", [True, False])
+@pytest.mark.parametrize("in_place", [
+    # the in-place mode (ZFEC_HIP_ZC_WIDE_LIMIT > 0, off by default) has not
+    # run on a GPU box yet: enable it together with the knob's default
+    pytest.param(True, marks=pytest.mark.skip(reason="ZFEC_HIP_ZC_WIDE_LIMIT is off by default and not yet "
+                                                     "validated on a GPU box (DESIGN.md section 9, item 8)")),
+    False])
 def test_wide_small_calls_bounce_modes(in_place, knobs):
     """Small calls of wide codes from bytes: with ZFEC_HIP_ZC_WIDE_LIMIT=256 KiB
     the kernel reads and writes the pinned bounce buffer in place over PCIe up
