@@ -16,7 +16,12 @@ summed over GPUs, / wall time of the K timed steps (max over ranks), GB/s
 capture them once into a HIP graph and replay it per step; on ROCm 7.2 the
 replay measured slower than eager launches).
 
-Multi-GPU (torchrun, one rank per GPU): stripes are independent, so ranks
+Multi-GPU (one process per GPU): `python bench.py --gpus N` with no WORLD_SIZE
+in the environment starts N ranks itself (torch.distributed.run on 127.0.0.1,
+before this process makes any GPU call) and exits with their status; under an
+external torchrun WORLD_SIZE must equal --gpus, or the run stops with an error
+instead of measuring another number of GPUs.  The line's `ranks_seen` is the
+world size the process group reported.  Stripes are independent, so ranks
 never exchange data.  cfg2/cfg3: each rank owns its own stripe (weak
 scaling); with --slabs the ONE stripe's block byte range is split instead
 (zfec_amd.shard.slab_range, strong scaling: rank r holds columns [c0, c1) of
@@ -35,14 +40,53 @@ restatement (kind "port").
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv):
+    """--gpus N without WORLD_SIZE: run this script as N ranks (one process per
+    GPU, as the driver's torchrun line does) and return their exit status; None
+    when this process is a rank already (or N is 1).  Runs before torch or the
+    library is imported, so the parent never touches a GPU."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args(argv)[0].gpus
+    if n < 1:
+        sys.exit("bench.py: --gpus must be >= 1 (got %d)" % n)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d: refusing to measure another number of GPUs than asked"
+                     % (ws, n))
+        return None
+    if n == 1:
+        return None
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, cwd=ROOT)
+
+
+if __name__ == "__main__":
+    _rc = launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 import zfec_amd  # noqa: E402
@@ -105,15 +149,20 @@ def parse():
     p.add_argument("--paired", action="store_true",
                    help="each step as ONE fec_run_batch_jobs call on one stream: its encode and decode share one "
                         "matapply_pair launch where both are register-kernel shapes (cfg2), else one launch each")
+    p.add_argument("--dry-run", action="store_true",
+                   help="set up the ranks and the process group (gloo, no GPU call), print rank 0's view of the world "
+                        "as one JSON line and exit: the launch path, testable on CPU")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a captured HIP graph (measured slower than eager launches on ROCm 7.2)")
     return p.parse_args()
 
 
-def dist_setup():
+def dist_setup(gpus=1):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:  # launch_ranks checked this already; keep the invariant for importers
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, gpus))
     # ZFEC_BENCH_DIST=1 initialises the process group at world size 1 too, so
     # the RCCL path (init, barrier, max/sum reductions) can be rehearsed under
     # torchrun on a one-GPU box
@@ -127,6 +176,10 @@ def dist_setup():
             torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
             dist.init_process_group("gloo")
         else:
+            ndev = torch.cuda.device_count()
+            if local >= ndev:
+                raise SystemExit("bench.py: rank %d (LOCAL_RANK %d) has no GPU of its own: %d visible; one rank "
+                                 "per GPU over RCCL" % (rank, local, ndev))
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return dist, rank, world
@@ -245,36 +298,61 @@ def pmc_traffic(workload, leg="encode cold"):
 VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4.25
 
 
+# Device code the committed counter summaries describe: a summary is used only
+# when it was collected on these exact sources (tools/pmc_sq_summary.py).
+DEVICE_SOURCES = ("zfec_amd/csrc/kernels.hip", "zfec_amd/csrc/kernels.hpp", "zfec_amd/csrc/bitslice.cpp",
+                  "zfec_amd/csrc/bitslice.hpp")
+
+
+def device_tree_hash():
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in DEVICE_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def _same_kernel(traced, printed):
-    """rocprof's demangled template name vs the library's short variant name."""
+    """rocprof's demangled name vs the library's name: the same name, or the
+    library's short template name as the leading arguments of the traced one
+    (matapply_reg<3,7> vs matapply_reg<3, 7, 3, true, true>)."""
     if traced == printed:
         return True
     if "<" not in traced or "<" not in printed or traced.split("<")[0] != printed.split("<")[0]:
         return False
-    nums = [a.strip() for a in traced.split("<", 1)[1].rstrip(">").split(",") if a.strip().isdigit()]
-    pargs = [a.strip() for a in printed.split("<", 1)[1].rstrip(">").split(",") if a.strip().isdigit()]
-    return nums[:len(pargs)] == pargs
+    targs = [a.strip() for a in traced.split("<", 1)[1].rsplit(">", 1)[0].split(",")]
+    pargs = [a.strip() for a in printed.split("<", 1)[1].rsplit(">", 1)[0].split(",")]
+    return targs[:len(pargs)] == pargs
 
 
 def valu_roofline(workload, kernel, launch_ms):
     """Second roofline of the dominant kernel: VALU wave-instructions per launch
     (SQ_INSTS_VALU from the committed counter summary, tools/pmc_sq.sh) over the
-    launch duration, against the VALU issue ceiling."""
+    launch duration, against the VALU issue ceiling.  Only from a summary
+    collected on this tree's device sources, and only when exactly one traced
+    kernel of the workload is this one."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_sq_summary.json")) as f:
-            d = json.load(f)["workloads"].get(workload, {})
+            summ = json.load(f)
+        d = summ["workloads"].get(workload, {})
     except (OSError, ValueError, KeyError):
         return None
-    for name, c in d.items():
-        if _same_kernel(name, kernel) and c.get("SQ_INSTS_VALU"):
-            n = float(c["SQ_INSTS_VALU"])
-            ach = n / (launch_ms * 1e-3)
-            return {"bound": "valu-issue", "insts_per_launch": int(n), "achieved": round(ach / 1e9, 1),
-                    "peak": round(VALU_PEAK_INSTS / 1e9, 1), "unit": "G VALU wave-instructions/s",
-                    "frac": round(ach / VALU_PEAK_INSTS, 4),
-                    "basis": "SQ_INSTS_VALU per dispatch (profiles/pmc_sq_summary.json) / launch_ms; peak = "
-                             "1024 SIMDs x 2.4 GHz / 4.25 cycles per VOP3 wave-instruction (measured)"}
-    return None
+    if summ.get("tree") != device_tree_hash():
+        return {"error": "profiles/pmc_sq_summary.json was collected on other device sources (tree %s, this tree %s)"
+                         % (summ.get("tree"), device_tree_hash())}
+    hits = [(n, c) for n, c in d.items() if _same_kernel(n, kernel) and c.get("SQ_INSTS_VALU")]
+    if len(hits) != 1:
+        return {"error": "%d traced kernels match %s" % (len(hits), kernel)}
+    name, c = hits[0]
+    n = float(c["SQ_INSTS_VALU"])
+    ach = n / (launch_ms * 1e-3)
+    return {"bound": "valu-issue", "insts_per_launch": int(n), "achieved": round(ach / 1e9, 1),
+            "peak": round(VALU_PEAK_INSTS / 1e9, 1), "unit": "G VALU wave-instructions/s",
+            "frac": round(ach / VALU_PEAK_INSTS, 4), "traced_kernel": name, "tree": summ.get("tree"),
+            "basis": "SQ_INSTS_VALU per dispatch (profiles/pmc_sq_summary.json, same device sources) / launch_ms; "
+                     "peak = 1024 SIMDs x 2.4 GHz / 4.25 cycles per VOP3 wave-instruction (measured)"}
 
 
 def host_cpus():
@@ -799,9 +877,31 @@ def run_batched_1mib(steps):
     return res
 
 
+def dry_run(args):
+    """--dry-run: the ranks and their process group, no GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=int(os.environ.get("RANK", "0")), world_size=world,
+                            init_method=None if world > 1 else "tcp://127.0.0.1:%d" % _free_port())
+    t = torch.tensor([1.0])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": dist.get_world_size(),
+                          "ranks_reduced": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    dist, rank, world = dist_setup()
+    if args.dry_run:
+        return dry_run(args)
+    dist, rank, world = dist_setup(args.gpus)
+    ranks_seen = dist.get_world_size() if dist is not None else 1
+    if ranks_seen != args.gpus:
+        raise SystemExit("bench.py: the process group has %d ranks, --gpus %d" % (ranks_seen, args.gpus))
     k, m, stripe, nstripes, scaling = WORKLOADS[args.workload]
     r = m - k
     sz = -(-stripe // k)
@@ -849,6 +949,7 @@ def main():
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 4),

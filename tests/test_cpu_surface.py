@@ -386,6 +386,38 @@ def test_reuse_host_memory_opt_in():
     assert "reuse_host_memory" in zfec_amd.__all__
 
 
+_MALLOPT_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from zfec_amd import _fec
+blocks = [bytes(2 << 20)] * 3
+for _ in range(2):
+    try:
+        _fec.Encoder(3, 10).encode(blocks)
+    except _fec.Error:
+        pass  # no GPU here: the call fails after the allocator hook ran
+print("mallopt_calls=%d" % _fec._mallopt_calls())
+"""
+
+
+@pytest.mark.parametrize("policy", [None, "default", "reuse"])
+def test_bytes_calls_leave_allocator_policy_alone(policy):
+    """A 2 MiB-block `bytes` encode changes glibc's allocator policy only when
+    the caller opts in with ZFEC_AMD_MALLOC=reuse (the reference module never
+    calls mallopt, zfec/_fecmodule.c:206-217); by default nothing is set."""
+    import sys
+
+    env = dict(os.environ)
+    env.pop("ZFEC_AMD_MALLOC", None)
+    if policy:
+        env["ZFEC_AMD_MALLOC"] = policy
+    res = subprocess.run([sys.executable, "-c", _MALLOPT_CHILD, ROOT], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr[-2000:]
+    want = 2 if policy == "reuse" else 0
+    assert ("mallopt_calls=%d" % want) in res.stdout, res.stdout + res.stderr[-2000:]
+
+
 def test_package_exports_like_reference():
     """`import zfec` makes Encoder, Decoder, Error, __version__ and the modules
     easyfec, filefec, cmdline_zfec, cmdline_zunfec available

@@ -34,12 +34,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _torchrun(args):
+def _torchrun(args, launcher=True):
+    """launcher=False: a plain `python bench.py --gpus 2`, which starts its two
+    ranks itself (bench.py launch_ranks), as the driver's command shape does."""
     env = dict(os.environ)
     env["ZFEC_BENCH_BACKEND"] = "gloo"
     env.setdefault("OMP_NUM_THREADS", "4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args
+    if launcher:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+               "127.0.0.1", "--master-port", str(_free_port())] + cmd[1:]
     res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=ROOT)
     assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
@@ -51,7 +57,7 @@ def _torchrun(args):
 def test_bench_two_ranks_cfg4_sharded():
     out = _torchrun(["--workload", "cfg4", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-extra", "--fresh",
                      "0"])
-    assert out["n_gpus"] == 2
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
     assert out["config"]["stripes_per_gpu"] == 512  # 1024 stripes split over 2 ranks
     assert out["scaling"] == "strong"
     assert math.isfinite(out["value"]) and out["value"] > 0
@@ -66,4 +72,15 @@ def test_bench_two_ranks_cfg2_slabs():
     sz = -(-(64 << 20) // 3)
     # rank 0's slab: the first half of every block, on a 256-byte boundary
     assert out["config"]["slab_bytes_rank0"] == -(-(-(-sz // 256)) // 2) * 256
+    assert math.isfinite(out["value"]) and out["value"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_flag_launches_its_ranks():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts the two
+    ranks itself, and the line reports the world the process group saw."""
+    out = _torchrun(["--workload", "cfg4", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-extra", "--fresh", "0"],
+                    launcher=False)
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
+    assert out["config"]["stripes_per_gpu"] == 512
     assert math.isfinite(out["value"]) and out["value"] > 0

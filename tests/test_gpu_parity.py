@@ -244,13 +244,12 @@ def test_c_abi_host_memory_flag():
         assert (rec == data[[0, 2]]).all(), sz
 
 
-@pytest.mark.parametrize("env", [{"ZFEC_HIP_POOL_COPY_MIN": "0"}, {"ZFEC_HIP_STAGE_MIN": str(1 << 60)},
-                                 {"ZFEC_HIP_STAGE_MIN": "0"}])
+@pytest.mark.parametrize("env", [{}, {"ZFEC_HIP_STAGE_MIN": str(1 << 60)}, {"ZFEC_HIP_STAGE_MIN": "0"}])
 def test_host_small_call_paths(env, knobs):
-    """Host calls under 4 MiB: the pinned bounce buffer with its copies on the
-    host pool, the bounce buffer up to 4 MiB (staged path off), and the staged
-    path from any size (blocks >= 64 KiB) -- each bit-exact against the oracle,
-    encode and a mixed primary/secondary decode."""
+    """Host calls under 4 MiB: as shipped, the bounce buffer up to 4 MiB
+    (staged path off), and the staged path from any size (blocks >= 64 KiB) --
+    each bit-exact against the oracle, encode and a mixed primary/secondary
+    decode."""
     knobs(**env)
     k, m = 3, 10
     rng = np.random.default_rng(77)
@@ -543,25 +542,18 @@ def _run_child(spec, env_extra, tmp_path, tag):
 
 @pytest.mark.parametrize("layout", sorted(_LAYOUTS))
 def test_batch_layout_env_variants(layout, tmp_path):
-    """The same fec_encode_batch run five ways, each in its own process (the
-    knobs are read once per process): as shipped, with the block-major collapse
-    off (ZFEC_HIP_BATCH_COLLAPSE=0), with at most 1024 units per launch
-    (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte ranges, batches
-    into stripe groups), and with the register kernels' store policy forced to
-    nt and to nt sc1 (ZFEC_HIP_STORE).  All outputs, guard bytes included,
+    """The same fec_encode_batch run two ways, each in its own process (the
+    knobs are read once per process): as shipped, and with at most 1024 units
+    per launch (ZFEC_HIP_LAUNCH_UNITS=1024: long rows are cut into byte
+    ranges, batches into stripe groups).  Both outputs, guard bytes included,
     must be identical, and sampled stripes must equal the oracle's parity."""
     import importlib.util
     import os
 
     spec = _LAYOUTS[layout]
     base, kern = _run_child(spec, {}, tmp_path, "base")
-    nocol, _ = _run_child(spec, {"ZFEC_HIP_BATCH_COLLAPSE": "0"}, tmp_path, "nocollapse")
     split, _ = _run_child(spec, {"ZFEC_HIP_LAUNCH_UNITS": "1024"}, tmp_path, "split")
-    assert np.array_equal(base, nocol), "collapse changed the output"
     assert np.array_equal(base, split), "launch splitting changed the output"
-    for pol in ("nt", "ntsc1"):
-        got, _ = _run_child(spec, {"ZFEC_HIP_STORE": pol}, tmp_path, "store_" + pol)
-        assert np.array_equal(base, got), "store policy %s changed the output" % pol
     if layout == "rows_object_major":
         assert "matapply_rows" in kern, kern
     child = importlib.util.spec_from_file_location(
@@ -1196,17 +1188,14 @@ def test_small_call_signal_under_load():
     assert not errors, errors
 
 
-@pytest.mark.parametrize("inline", [True, False])
-def test_small_call_compact_kernel(inline, knobs):
+def test_small_call_compact_kernel():
     """Synchronous calls from bytes with k <= 4, r <= 8 and blocks of at most
     4 KiB run on the compact one-workgroup kernel (kernels.hip matapply_one,
     whole 16-byte units in the bounce buffer; inputs inside the argument
-    block where k x sz fits 4,352 bytes, or read from the bounce buffer with
-    ZFEC_HIP_SMALL_INLINE=0): bit-exact against the oracle for every such
-    (k, r) at sizes around the unit and the 4 KiB limit; one byte past the
-    limit takes the general kernels."""
-    if not inline:
-        knobs(ZFEC_HIP_SMALL_INLINE="0")
+    block where k x sz fits 4,352 bytes, else read from the bounce buffer):
+    bit-exact against the oracle for every such (k, r) at sizes around the
+    unit and the 4 KiB limit, both forms; one byte past the limit takes the
+    general kernels."""
     rng = np.random.default_rng(77)
     for k in range(1, 5):
         for m in range(k + 1, k + 9):
@@ -1216,7 +1205,7 @@ def test_small_call_compact_kernel(inline, knobs):
                 out = enc.encode([data[i].tobytes() for i in range(k)])
                 name = capi.last_kernel_name()
                 ksz = min((sz + 255) // 256 * 256, (sz + 127) // 128 * 128)
-                want = "matapply_one<%d,inline>" % k if inline and k * ksz <= 4352 else "matapply_one<%d>" % k
+                want = "matapply_one<%d,inline>" % k if k * ksz <= 4352 else "matapply_one<%d>" % k
                 assert (name == want) == (sz <= 4096), (k, m, sz, name, want)
                 par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
                 assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
@@ -1290,25 +1279,22 @@ def test_medium_call_wait_modes(mode, knobs):
             assert b"".join(rec) == data.tobytes(), (k, m, stripe)
 
 
-@pytest.mark.parametrize("in_place", [
-    # the in-place mode (ZFEC_HIP_ZC_WIDE_LIMIT > 0, off by default) has not
-    # run on a GPU box yet: enable it together with the knob's default
-    pytest.param(True, marks=pytest.mark.skip(reason="ZFEC_HIP_ZC_WIDE_LIMIT is off by default and not yet "
-                                                     "validated on a GPU box (DESIGN.md section 9, item 8)")),
-    False])
-def test_wide_small_calls_bounce_modes(in_place, knobs):
-    """Small calls of wide codes from bytes: with ZFEC_HIP_ZC_WIDE_LIMIT=256 KiB
-    the kernel reads and writes the pinned bounce buffer in place over PCIe up
-    to that many host bytes; with 0 (the default) one H2D and one D2H copy
-    move them.  Bit-exact against the oracle in both modes, encode and decode."""
-    knobs(ZFEC_HIP_ZC_WIDE_LIMIT=str(256 << 10) if in_place else "0")
+def test_wide_small_calls_bounce_modes():
+    """Small calls of wide codes from bytes: up to 256 KiB of host blocks the
+    kernel reads and writes the pinned bounce buffer in place over PCIe (the
+    stream then publishes completion in the pinned word, fec_last_wait 1);
+    past that one H2D and one D2H copy move them (hipStreamSynchronize, 0).
+    Bit-exact against the oracle either way, encode and decode."""
     rng = np.random.default_rng(2060)
     for k, m in ((20, 60), (10, 16), (5, 9), (3, 12)):
         enc, dec = zfec_amd.Encoder(k, m), zfec_amd.Decoder(k, m)
-        for stripe in (1, 4096, 20000, 65536):
+        for stripe in (1, 4096, 20000, 65536, 131072):
             sz = -(-stripe // k)
             data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
             out = enc.encode([data[i].tobytes() for i in range(k)])
+            in_place = sz * m <= 256 << 10
+            if not (k <= 4 and m - k <= 8):  # the register kernels' calls have their own tests
+                assert capi.last_wait() == (1 if in_place else 0), (k, m, stripe)
             par = np.stack([np.frombuffer(b, np.uint8) for b in out[k:]])
             assert (par == oracle.encode(k, m, data)).all(), (k, m, stripe, in_place)
             nums = list(range(m - k, m))

@@ -4,6 +4,7 @@ and the per-rank results gathered back equal the single-process result.  The
 per-stripe work here is the CPU oracle (this suite has no GPU); on the GPU
 box the same partition feeds fec_encode_batch per rank."""
 import hashlib
+import json
 import os
 import socket
 
@@ -13,6 +14,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from zfec_amd.shard import encode_shard, shard_range
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_shard_range_partition():
@@ -202,3 +205,38 @@ def test_rw_ceiling_bounds():
     assert abs(bench.rw_ceiling(0, 1, 1.0)["GBps"] - bench.HBM_WRITE_GBPS) < 0.1
     assert abs(c["achieved_frac_of_ceiling"] - 5000.0 / c["GBps"]) < 1e-3
     assert abs(c["frac_of_peak"] - c["GBps"] / bench.HBM_PEAK_GBPS) < 1e-3
+
+
+def _bench(args, env_extra=None):
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=240, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_gpus_flag_starts_that_many_ranks(n):
+    """`python bench.py --gpus N` (the driver's command shape) starts N ranks
+    itself when no launcher set WORLD_SIZE, and the process group has N ranks
+    (--dry-run: gloo, no GPU call)."""
+    res = _bench(["--gpus", str(n), "--dry-run"])
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["ranks_seen"] == n and out["ranks_reduced"] == n
+
+
+def test_bench_world_size_mismatch_fails_loudly():
+    """Under a launcher whose WORLD_SIZE differs from --gpus, bench.py exits
+    non-zero before any GPU work instead of measuring another number of GPUs."""
+    res = _bench(["--gpus", "3", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert res.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 3" in res.stderr
+    res = _bench(["--gpus", "0"])
+    assert res.returncode != 0

@@ -12,14 +12,21 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def summarize(tag, workloads):
+    from bench import device_tree_hash
+
     out = {"source": "tools/pmc_sq.sh %s %s (rocprofv3 --pmc, two passes, per-dispatch means)"
-                     % ("|".join(workloads), tag), "workloads": {}}
+                     % ("|".join(workloads), tag),
+           "tree": device_tree_hash(),
+           "tree_basis": "sha256 of the device sources (bench.py DEVICE_SOURCES) the counters were collected on; "
+                         "bench.py's valu_roofline uses this file only when it matches the tree it runs from",
+           "workloads": {}}
     for w in workloads:
         ws = {}
-        for sub in ("ic", "sq"):
+        for sub in ("ic", "sq", "lds"):
             files = glob.glob(os.path.join(ROOT, "gpurun_out", tag, w, sub, "**", "*counter_collection.csv"),
                               recursive=True)
             if not files:

@@ -217,18 +217,17 @@ std::string source_ksplit(const std::vector<uint8_t>& masks, unsigned k, unsigne
                           const char* name) {
     Src e;
     e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
-    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", opt.store_aux, opt.shift64 ? 1 : 0);
+    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", 2u, 1);  // nt stores; 64-bit-shift transposes
     e.s += kPrelude;
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
     e("extern \"C\" __global__ __launch_bounds__(256) void %s(const Args a) {\n", name);
     e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n  const u32 lane = threadIdx.x & 63u;\n");
     e("  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n");
-    const char* const PA = opt.argload ? "ka->" : "a.";
-    if (opt.argload)
-        e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
+    const char* const PA = "ka->";
+    e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
           "  const KArgs ka0 = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();\n");
     auto launder = [&](const char* indent) {
-        if (opt.argload) e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
+        e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
     };
     e("  __shared__ u32x4 red[%u];  // [row][wave][half][lane] partial planes\n", r * 4 * 2 * 64);
     e("  u32 s = blockIdx.x / a.cps, c = blockIdx.x - s * a.cps;\n");
@@ -256,7 +255,7 @@ std::string source_ksplit(const std::vector<uint8_t>& masks, unsigned k, unsigne
             e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", j, j, j, j, j, j, j, j);
             e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", j, j, j, j, j, j, j, j);
             emit_updates(e, masks, k, j, j, 0, r, init);
-            if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
+            e("    __builtin_amdgcn_sched_barrier(0);\n");
         }
         for (unsigned i = 0; i < r; ++i) {
             for (unsigned b = 0; b < 8; ++b)
@@ -290,7 +289,7 @@ std::string source_ksplit(const std::vector<uint8_t>& masks, unsigned k, unsigne
 
 std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const BsOptions& opt, const char* name) {
     field_init();
-    if (bitslice_ksplit(k, r, opt) && opt.probe == 0) {
+    if (bitslice_ksplit(k, r, opt)) {
         std::vector<uint8_t> masks(size_t(r) * k * 8);
         for (unsigned i = 0; i < r; ++i)
             for (unsigned j = 0; j < k; ++j) coef_masks(coef[i * k + j], &masks[(size_t(i) * k + j) * 8]);
@@ -305,31 +304,24 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
 
     Src e;
     e.s.reserve(size_t(r) * k * 8 * 40 + 8192);
-    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", opt.store_aux, opt.shift64 ? 1 : 0);
+    e("constexpr int kStoreAux = %u;\n#define ZFEC_SHIFT64 %d\n", 2u, 1);  // nt stores; 64-bit-shift transposes
     e.s += kPrelude;
-    if (opt.probe == 1)
-        e("__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs0(const u8* p) {\n"
-          "  return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(p), (short)0, 0, 0x00020000);\n}\n");
     e("struct Args {\n  u64 sz, iss, oss;\n  u32 nstripes, cps, gs_c, gs_s;\n  const u8* in[%u];\n  u8* out[%u];\n};\n", k, r);
     // split: the row tiles of a unit go to the waves of one workgroup, which
     // read the unit's inputs at the same time (L1/L2 hits instead of a re-read
     // from HBM per tile); otherwise each wave walks all tiles of its own unit.
     const bool split = bitslice_split(r, opt);
     const unsigned threads = split ? 64 * ntiles : 256;
-    if (opt.waves)
-        e("extern \"C\" __global__ __launch_bounds__(%u, %u) void %s(const Args a) {\n", threads, opt.waves, name);
-    else
-        e("extern \"C\" __global__ __launch_bounds__(%u) void %s(const Args a) {\n", threads, name);
+    e("extern \"C\" __global__ __launch_bounds__(%u) void %s(const Args a) {\n", threads, name);
     e("  const u32 lo16 = (threadIdx.x & 63u) * 16u;\n");
     // argload: block pointers are read from the kernel-argument segment where
     // they are used, through a pointer the compiler must treat as new in every
     // scope (empty asm), instead of all being loaded up front and spilled
-    const char* const PA = opt.argload ? "ka->" : "a.";
-    if (opt.argload)
-        e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
+    const char* const PA = "ka->";
+    e("  typedef __attribute__((address_space(4))) const Args* KArgs;\n"
           "  const KArgs ka0 = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();\n");
     auto launder = [&](const char* indent) {
-        if (opt.argload) e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
+        e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
     };
     if (split && opt.share) {
         e("  __shared__ u32x4 sh[%u];  // [input][half][lane] bit-planes of the unit\n", k * 128);
@@ -356,11 +348,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // share: each wave of the workgroup loads and transposes k / ntiles of the
     // unit's inputs once and leaves their bit-planes in LDS for all waves
     const bool share = split && opt.share;
-    // probe 1 (no HBM traffic): every buffer resource gets num_records = 0,
-    // so each load returns zeros and each store is dropped by the address
-    // check -- the same instruction stream, no memory traffic
-    const unsigned probe = opt.probe;
-    const char* const RS = probe == 1 ? "rs0" : "rs";
+    const char* const RS = "rs";
     auto emit_ld = [&](const char* ind, const char* dst, const char* rsrc, unsigned) {
         e("%sconst u32x4 %s_0 = ld(%s, lo16), %s_1 = ld(%s, lo16 + 1024u);\n", ind, dst, rsrc, dst, rsrc);
     };
@@ -396,8 +384,7 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                   j);
                 e("      u32 w%u_4 = p%u_1.x, w%u_5 = p%u_1.y, w%u_6 = p%u_1.z, w%u_7 = p%u_1.w;\n", j, j, j, j, j, j, j,
                   j);
-                if (probe != 2)
-                    e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
+                e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
                 e("      sh[%uu + lane] = u32x4{w%u_0, w%u_1, w%u_2, w%u_3};\n", j * 128, j, j, j, j);
                 e("      sh[%uu + lane] = u32x4{w%u_4, w%u_5, w%u_6, w%u_7};\n", j * 128 + 64, j, j, j, j);
             }
@@ -425,18 +412,6 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                 emit_load(n + pf);
             e("    u32 q%u_0 = l%u_0.x, q%u_1 = l%u_0.y, q%u_2 = l%u_0.z, q%u_3 = l%u_0.w;\n", n, n, n, n, n, n, n, n);
             e("    u32 q%u_4 = l%u_1.x, q%u_5 = l%u_1.y, q%u_6 = l%u_1.z, q%u_7 = l%u_1.w;\n", n, n, n, n, n, n, n, n);
-            if (probe == 2) {  // no arithmetic: one XOR per plane into the tile's first row
-                for (unsigned b = 0; b < 8; ++b) {
-                    char& ini = init[b];
-                    if (!ini)
-                        e("    a%u_%u = q%u_%u;\n", r0, b, n, b);
-                    else
-                        e("    a%u_%u ^= q%u_%u;\n", r0, b, n, b);
-                    ini = 1;
-                }
-                if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
-                continue;
-            }
             if (!share)  // LDS holds planes already
                 e("    tr8(q%u_0, q%u_1, q%u_2, q%u_3, q%u_4, q%u_5, q%u_6, q%u_7);\n", n, n, n, n, n, n, n, n);
             Combos lo{n, 'L', 0}, hi{n, 'H', 4};
@@ -465,52 +440,15 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
                     e("    %s ^= %s;\n", acc, u.ml ? sl.c_str() : sh.c_str());
                 }
             };
-            if (!opt.gray) {  // combinations on first use, in row order
-                for (const Upd& u : ups)
-                    update(u, u.ml ? lo.name(u.ml, e) : std::string(), u.mh ? hi.name(u.mh, e) : std::string());
-            } else {
-                // H combinations stay live for the step; L values are walked in
-                // Gray-code order (one XOR from the previous one), so only the
-                // current one is live while the updates that use it run
-                for (const Upd& u : ups)
-                    if (!u.ml) update(u, std::string(), hi.name(u.mh, e));
-                static const unsigned kGray[15] = {1, 3, 2, 6, 7, 5, 4, 12, 13, 15, 14, 10, 11, 9, 8};
-                int last = -1;
-                for (int g = 0; g < 15; ++g)
-                    for (const Upd& u : ups)
-                        if (u.ml == kGray[g]) last = g;
-                std::string prev;
-                for (int g = 0; g <= last; ++g) {
-                    const unsigned m = kGray[g];
-                    std::string cur;
-                    char nm[32];
-                    if ((m & (m - 1)) == 0) {
-                        snprintf(nm, sizeof nm, "q%u_%u", n, unsigned(__builtin_ctz(m)));
-                        cur = nm;
-                    } else {
-                        const unsigned bit = m ^ kGray[g - 1];
-                        snprintf(nm, sizeof nm, "G%u_%u", n, m);
-                        e("    const u32 %s = %s ^ q%u_%u;\n", nm, prev.c_str(), n, unsigned(__builtin_ctz(bit)));
-                        cur = nm;
-                    }
-                    for (const Upd& u : ups)
-                        if (u.ml == m) update(u, cur, u.mh ? hi.name(u.mh, e) : std::string());
-                    prev = cur;
-                }
-            }
-            if (opt.barriers) e("    __builtin_amdgcn_sched_barrier(0);\n");
+            // combinations on first use, in row order
+            for (const Upd& u : ups)
+                update(u, u.ml ? lo.name(u.ml, e) : std::string(), u.mh ? hi.name(u.mh, e) : std::string());
+            e("    __builtin_amdgcn_sched_barrier(0);\n");
         }
         for (unsigned i = r0; i < r1; ++i) {
-            if (probe == 2 && i > r0) {
-                e("    a%u_0 = a%u_0 ^ %uu;", i, r0, i);
-                for (unsigned b = 1; b < 8; ++b) e(" a%u_%u = a%u_%u;", i, b, r0, b);
-                e("\n");
-            } else {
-                for (unsigned b = 0; b < 8; ++b)
-                    if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
-            }
-            if (probe != 2)
-                e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
+            for (unsigned b = 0; b < 8; ++b)
+                if (!init[size_t(i - r0) * 8 + b]) e("    a%u_%u = 0u;\n", i, b);
+            e("    tr8(a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7);\n", i, i, i, i, i, i, i, i);
             e("    const __amdgpu_buffer_rsrc_t ro%u = %s(%sout[%u] + uo);\n", i, RS, PA, i);
             e("    st(ro%u, lo16, u32x4{a%u_0, a%u_1, a%u_2, a%u_3});\n", i, i, i, i, i);
             e("    st(ro%u, lo16 + 1024u, u32x4{a%u_4, a%u_5, a%u_6, a%u_7});\n", i, i, i, i, i);
@@ -734,7 +672,7 @@ std::atomic<int> g_mode{-1};
 // Options of a kernel for an r x k matrix: the configured ones, with the
 // planes shared through LDS only while all k inputs' planes fit (2 KiB each).
 BsOptions options_for(unsigned k) {
-    BsOptions o = config().jit;
+    BsOptions o;
     if (k > 32) o.share = false;
     return o;
 }
@@ -745,14 +683,13 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     std::string key;
     key.reserve(64 + size_t(k) * r);
     char hdr[80];
-    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/%d/%u/%d/%u/%d/", k, r, opt.max_tile, opt.prefetch, opt.barriers ? 1 : 0,
-             opt.store_aux, opt.gray ? 1 : 0, opt.waves, opt.split ? 1 : 0);
+    // (the layout of the earlier, configurable option set: kernel names, and
+    // with them the code objects cached in jit_cache/, stay the same)
+    snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/1/2/0/0/%d/", k, r, opt.max_tile, opt.prefetch, opt.split ? 1 : 0);
     key += hdr;
-    if (opt.argload) key += "argload/";
-    if (opt.shift64) key += "shift64/";
+    key += "argload/shift64/";
     if (opt.share && bitslice_split(r, opt)) key += "share/";
-    if (opt.probe) key += "probe" + std::to_string(opt.probe) + "/";
-    if (bitslice_ksplit(k, r, opt) && !opt.probe) key += "ksplit/";
+    if (bitslice_ksplit(k, r, opt)) key += "ksplit/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;
 }
@@ -768,7 +705,7 @@ Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::un
     char nm[80];
     snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
     e->name = nm;
-    const bool ks = bitslice_ksplit(k, r, opt) && opt.probe == 0;
+    const bool ks = bitslice_ksplit(k, r, opt);
     e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
     e->units_per_block = bitslice_split(r, opt) || ks ? 1 : 4;
     R.entries.emplace(key, std::move(ne));
@@ -965,7 +902,7 @@ hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const cha
     for (unsigned i = 0; i < r; ++i) args[5 + k + i] = reinterpret_cast<uint64_t>(a.out[i]);
     size_t size = (5 + k + r) * sizeof(uint64_t);
     void* conf[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
-    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, cfg->jit_lds, stream, nullptr, conf);
+    const hipError_t er = hipModuleLaunchKernel(L.fn, grid, 1, 1, threads, 1, 1, 0, stream, nullptr, conf);
     if (er == hipSuccess && name_out) *name_out = name;
     return er;
 }

@@ -28,23 +28,20 @@ namespace zfec_hip {
 constexpr int kBsChunk = 2048;    // bytes of a block per wave per unit (32 per lane, two 1 KiB halves)
 constexpr int kBsMaxTile = 10;    // output rows per register tile (8 accumulator planes each)
 
+// The generator's shape choices.  Fixed: the variants that lost their A/Bs
+// (Gray-code combination order, launch-bound hints, tile heights, no prefetch,
+// no scheduling barriers, pointers loaded up front, 32-bit-shift transposes,
+// other store policies; DESIGN.md §4 and the committed profiles/r0*_jit_*
+// logs) were removed in round 4, and so were the measurement-only probe
+// variants, whose outputs were not the code's.  Only the LDS sharing of the
+// planes depends on the matrix (options_for: k <= 32).
 struct BsOptions {
     unsigned max_tile = kBsMaxTile;  // rows per tile (tiles are near-equal)
     unsigned prefetch = 2;           // input steps loaded ahead of the one being computed
-    bool barriers = true;            // sched_barrier between input steps (keeps the prefetch shape)
-    unsigned store_aux = 2;          // cache policy bits of the output stores (2 = nt)
-    bool gray = false;               // walk the planes-0-3 combinations in Gray-code order
-    unsigned waves = 0;              // __launch_bounds__ waves-per-SIMD hint (0: none)
     bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
     bool share = true;               // split: inputs transposed once per unit, bit-planes shared through LDS
-    bool argload = true;             // block pointers loaded where used (no up-front SGPR spill)
-    bool shift64 = true;             // bit transposes shift register pairs with 64-bit shifts (4-9 % fewer
-                                     // VALU; cfg4 decode 380 -> 375 us, encode unchanged: profiles/r02_jit_shift64.log)
     bool ksplit = true;              // one row tile and k > 32: a unit's inputs split over the 4 waves of a
                                      // workgroup, partial planes reduced through LDS (4x the waves per unit)
-    unsigned probe = 0;              // measurement variants (tools/jit_probe.py; results NOT the code's):
-                                     // 1 = no HBM traffic (inputs synthesised, stores dropped),
-                                     // 2 = no arithmetic (same loads and stores, outputs = XOR of raw inputs)
 };
 
 // Largest matrix (k * r coefficients per launch) the generator specialises:

@@ -418,46 +418,8 @@ constexpr size_t kStageMinBlock = size_t(64) << 10;
 // KB K=3/M=10 stripes from bytes (tools/small_ab_inproc.py --set zc,
 // profiles/r03_zc_ab.log): encode 44.5-51.3 -> 25.1-33.0 us, decode
 // 17.0-38.3 -> 16.9-19.8 us against one H2D and one D2H copy.
-// Small calls: from Config::pool_copy_min bytes per direction the
-// bounce-buffer copies run on the host pool.  Off by default: waking the pool
-// costs more than it saves below 4 MiB (1 MiB K=3/M=10 stripe: 255 us pooled
-// vs 209 us on the calling thread, profiles/r02_host_lat_ab.log).
 
 constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// ZFEC_HIP_TRACE_HOST=1: per-phase times of a large pageable call on stderr.
-struct HostTrace {
-    bool on;
-    std::chrono::steady_clock::time_point t;
-    std::string line;
-    HostTrace() : on(config().trace_host), t(std::chrono::steady_clock::now()) {}
-    // accumulated waits inside a loop: lap() starts one, add(i) ends it into slot i
-    std::chrono::steady_clock::time_point l;
-    double acc[3] = {0, 0, 0};
-    void lap() {
-        if (on) l = std::chrono::steady_clock::now();
-    }
-    void add(int i) {
-        if (on) acc[i] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - l).count();
-    }
-    void sums(const char* a, const char* b, const char* c) {
-        if (!on) return;
-        char buf[160];
-        snprintf(buf, sizeof buf, " [%s %.0f %s %.0f %s %.0f]", a, acc[0], b, acc[1], c, acc[2]);
-        line += buf;
-    }
-    void mark(const char* what) {
-        if (!on) return;
-        const auto n = std::chrono::steady_clock::now();
-        char b[64];
-        snprintf(b, sizeof b, " %s %.0f", what, std::chrono::duration<double, std::micro>(n - t).count());
-        line += b;
-        t = n;
-    }
-    ~HostTrace() {
-        if (on) fprintf(stderr, "zfec_hip host path (us):%s\n", line.c_str());
-    }
-};
 
 // Kernel-visible address of the host block [p, p + n), or nullptr unless the
 // whole block is page-locked (first and last byte mapped at the same offset).
@@ -521,7 +483,6 @@ int ensure_sbuf(DevCtx& d, size_t bytes) {
 // caller-locked blocks are read / written in place.
 int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* const* in, gf* const* out,
                size_t sz, Marshal& m, hipStream_t st) {
-    HostTrace tr;
     std::vector<char> host_in(k, 0), host_out(r, 0);
     std::vector<const uint8_t*> base_in(m.zin);  // kernel-visible bases of device / caller-locked blocks
     std::vector<uint8_t*> base_out(m.zout);
@@ -551,7 +512,6 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     HostPool& pool = HostPool::get();
     CopyLatch lin[kStageSlots], lout[kStageSlots];
     const size_t nchunks = (sz + C - 1) / C;
-    tr.mark("classify");
 
     auto stage_in = [&](size_t c) {
         const int s = static_cast<int>(c % kStageSlots);
@@ -584,11 +544,8 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     for (size_t c = 0; c < nchunks; ++c) {
         const int s = static_cast<int>(c % kStageSlots);
         const size_t off = c * C, len = std::min(C, sz - off);
-        tr.lap();
         pool.wait(&lin[s]);  // this chunk's inputs are in the slot
-        tr.add(0);
         pool.wait(&lout[s]);  // the slot's previous outputs have been copied out
-        tr.add(1);
         for (unsigned j = 0; j < k; ++j) zin[j] = base_in[j] + off;
         for (unsigned i = 0; i < r; ++i) zout[i] = base_out[i] + off;
         for (size_t q = 0; q < nin; ++q) zin[sin[q]] = ds + s * slot_bytes + q * C;
@@ -602,9 +559,7 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
         }
         if (c >= 1) {
             const int sp = static_cast<int>((c - 1) % kStageSlots);
-            tr.lap();
             e = hipEventSynchronize(d.ev_stg[sp]);
-            tr.add(2);
             if (e != hipSuccess)
                 return drain(hip_fail(e, "hipEventSynchronize"));
             copy_out(c - 1);
@@ -612,14 +567,11 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
     }
     if ((e = hipEventSynchronize(d.ev_stg[(nchunks - 1) % kStageSlots])) != hipSuccess)
         return drain(hip_fail(e, "hipEventSynchronize"));
-    tr.mark("kernels");
-    tr.sums("wait-in", "wait-out", "wait-kernel");
     copy_out(nchunks - 1);
     } catch (const std::exception& x) {
         return drain(set_status(FEC_ENOMEM, "staged host path: %s", x.what()));
     }
     drain(FEC_OK);
-    tr.mark("copy-out");
     return set_status(FEC_OK);
 }
 
@@ -636,7 +588,6 @@ int run_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf*
 int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, const gf* src, size_t sbs, size_t sss,
                      bool src_host, gf* dst, size_t dbs, size_t dss, bool dst_host, size_t sz, size_t ns,
                      hipStream_t st) {
-    HostTrace tr;
     const bool in_bm = sss == sz, out_bm = dss == sz;
     const size_t per = (src_host ? size_t(k) * sz : 0) + (dst_host ? size_t(r) * sz : 0);
     size_t gs = std::max<size_t>(1, (size_t(16) << 20) / std::max<size_t>(1, per));
@@ -723,7 +674,6 @@ int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, con
     std::vector<const uint8_t*> zin(k);
     std::vector<uint8_t*> zout(r);
     hipError_t e;
-    tr.mark("classify");
     try {  // a failed allocation while queueing copies: drain what was queued
     stage_in(0);
     for (size_t g = 0; g < ngroups; ++g) {
@@ -756,13 +706,11 @@ int run_batch_staged(DevCtx& d, const uint8_t* coef, unsigned k, unsigned r, con
     }
     if ((e = hipEventSynchronize(d.ev_stg[(ngroups - 1) % kStageSlots])) != hipSuccess)
         return drain(hip_fail(e, "hipEventSynchronize"));
-    tr.mark("kernels");
     copy_out(ngroups - 1);
     } catch (const std::exception& x) {
         return drain(set_status(FEC_ENOMEM, "staged batch path: %s", x.what()));
     }
     drain(FEC_OK);
-    tr.mark("copy-out");
     return set_status(FEC_OK);
 }
 
@@ -829,7 +777,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // 78-97 against 84-86 us (box-dependent: staged from 1.5 MiB) and decode
     // (1.05 MB) 49-56 against 61 us; 1 MiB stripes 186 against 159 us
     // (tools/small_ab_inproc.py --set stage, profiles/r03_stage_ab.log).
-    const bool zc_shape = (k <= 4 && r <= 8) || cfg.zc_wide;
+    const bool zc_shape = k <= 4 && r <= 8;
     const size_t stage_from = zc_shape ? std::max(cfg.stage_min, cfg.zc_limit) : cfg.stage_min;
     if (sz * nhost > cfg.pack_limit || (sz * nhost > stage_from && sz >= kStageMinBlock))
         return run_staged(*d, coef, k, r, in, out, sz, m, st);
@@ -846,22 +794,17 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     const size_t nin = m.in_host.size(), nout = m.out_host.size();
     if (ensure_hbuf(*d, slot * (nin + nout))) return t_status;
     uint8_t* hb = static_cast<uint8_t*>(d->hbuf);  // free: the previous call on this thread synchronised
-    // from Config::pool_copy_min bytes per direction the copies run on the
-    // host pool (256 KiB pieces), below it on this thread
-    const bool pooled = sz * std::max(nin, nout) >= cfg.pool_copy_min;
+    // the copies run on this thread (on the host pool they measured slower at
+    // every size this path serves: profiles/r02_host_lat_ab.log, r03_pool_ab.log)
     auto copy_blocks = [&](bool to_slot) {
-        CopyLatch latch;
         const size_t n = to_slot ? nin : nout;
         for (size_t q = 0; q < n; ++q) {
             uint8_t* sl = hb + slot * (to_slot ? q : nin + q);
-            void* dst = to_slot ? static_cast<void*>(sl) : static_cast<void*>(out[m.out_host[q]]);
-            const void* src = to_slot ? static_cast<const void*>(in[m.in_host[q]]) : static_cast<const void*>(sl);
-            if (pooled)
-                HostPool::get().copy_async(dst, src, sz, &latch, size_t(256) << 10);
+            if (to_slot)
+                std::memcpy(sl, in[m.in_host[q]], sz);
             else
-                std::memcpy(dst, src, sz);
+                std::memcpy(out[m.out_host[q]], sl, sz);
         }
-        if (pooled) HostPool::get().wait(&latch);
     };
     // Every block in the bounce buffer: its slots are 256-byte multiples, so
     // the kernel may run each row out to its next 128-byte line (whole 16-byte
@@ -871,23 +814,20 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // The compact one-workgroup kernel takes the inputs inside its argument
     // block where they fit (kernels.hip OneJobInline): no copy into the bounce
     // buffer, no PCIe reads in the kernel.
-    const bool one_shape = k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && cfg.small_one &&
-                           sz * nhost <= cfg.zc_limit;
-    const bool inline_in = one_shape && cfg.small_inline && nin == k && nhost == size_t(k) + r &&
-                           size_t(k) * ksz <= kOneInlineBytes;
+    const bool one_shape = k <= 4 && r <= 8 && ksz % 16 == 0 && ksz <= 4096 && sz * nhost <= cfg.zc_limit;
+    const bool inline_in = one_shape && nin == k && nhost == size_t(k) + r && one_inline_fits(k, ksz, sz);
     if (!inline_in) copy_blocks(true);
     // Zero-copy only for the register kernels (k <= 4, r <= 8), which issue
     // all their input loads at once: the wide-code kernels read inputs in
     // groups, each group a PCIe round trip of its own (K=20/M=60, 4 KiB stripe:
     // 40 us in the kernel over PCIe; tools/small_call_probe.py under
-    // rocprofv3, profiles/r02_small_calls.log).  ZFEC_HIP_ZC_WIDE=1 keeps
-    // them zero-copy (A/B runs).
-    // Wide codes in place for small packs (Config::zc_wide_limit, off by
-    // default until a GPU run validates it): K=20/M=60 from bytes, 4 KiB
-    // stripes encode in 20.5 us in place against 25.3 us with the copies, 64 KiB
-    // 44.7 against 47.9 us, but 128 KiB (393 KB of host blocks) 63.8 against
-    // 57.9 us (tools/small_ab_inproc.py --set zcwide, profiles/r03_zcwide_ab.log).
-    const bool zc_kernel = (k <= 4 && r <= 8) || cfg.zc_wide || sz * nhost <= cfg.zc_wide_limit;
+    // rocprofv3, profiles/r02_small_calls.log) -- except small packs, up to
+    // kZcWideLimit: K=20/M=60 from bytes, 4 KiB stripes encode in 20.5 us in
+    // place against 25.3 us with the copies, 64 KiB (197 KB of host blocks)
+    // 44.7 against 47.9 us, but 128 KiB (393 KB) 63.8 against 57.9 us
+    // (tools/small_ab_inproc.py --set zcwide, profiles/r03_zcwide_ab.log).
+    constexpr size_t kZcWideLimit = size_t(256) << 10;
+    const bool zc_kernel = (k <= 4 && r <= 8) || sz * nhost <= kZcWideLimit;
     bool signalled = false;
     const bool zero_copy = sz * nhost <= cfg.zc_limit && zc_kernel;
     if (zero_copy) {
@@ -1275,8 +1215,6 @@ void batch_geometry(unsigned k, unsigned r, size_t sbs, size_t sss, size_t dbs, 
     // both strides == sz) are one stripe of nstripes * sz bytes: output byte x
     // depends only on byte x of the inputs (zfec/fec.c:494-503, :547-556), so
     // one long-stream launch replaces the walk over short rows.
-    // (ZFEC_HIP_BATCH_COLLAPSE=0 turns this off, for A/B runs.)
-    const bool collapse = config().batch_collapse;
     // FEC_FLAG_ROW_PADDING: run the rows out to a whole 128-byte line where the
     // strides leave room.  A row ending mid-line leaves a partly written line
     // that HBM completes with a read-modify-write: 10^6 K=3/M=10 stripes of
@@ -1290,7 +1228,7 @@ void batch_geometry(unsigned k, unsigned r, size_t sbs, size_t sss, size_t dbs, 
                                                                                 dss >= (r - 1) * dbs + padded));
         if (room) grant = padded;
     }
-    if (collapse && nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
+    if (nstripes > 1 && sss == sz && dss == sz && sz <= SIZE_MAX / nstripes) {
         // the collapsed row may run out to its own next line only inside the
         // last stripe's grant: (nstripes - 1) * sz + grant
         const size_t len = sz * nstripes, padded = (len + 127) / 128 * 128;
@@ -1477,12 +1415,12 @@ FEC_API int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* st
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
     return guarded([&] {
         const unsigned call = flags & (FEC_FLAG_ASYNC | FEC_FLAG_LIBRARY_STREAM);
-        int devs[8];
+        int devs[64];
         size_t ndevs = 0;
         auto note_dev = [&](int dev) {
             for (size_t q = 0; q < ndevs; ++q)
                 if (devs[q] == dev) return;
-            if (ndevs < 8) devs[ndevs++] = dev;
+            if (ndevs < 64) devs[ndevs++] = dev;
         };
         size_t i = 0;
         while (i < njobs) {
@@ -1526,9 +1464,16 @@ FEC_API int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* st
             ++i;
         }
         if (!(flags & FEC_FLAG_ASYNC)) {
-            if (!(flags & FEC_FLAG_LIBRARY_STREAM)) {
+            if (!(flags & FEC_FLAG_LIBRARY_STREAM) && stream) {
                 const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+            } else if (!(flags & FEC_FLAG_LIBRARY_STREAM)) {
+                // the null stream: each job ran on its own device's null stream
+                for (size_t q = 0; q < ndevs; ++q) {
+                    DeviceGuard guard(devs[q]);
+                    const hipError_t e = hipStreamSynchronize(nullptr);
+                    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+                }
             } else {
                 for (size_t q = 0; q < ndevs; ++q) {
                     DeviceGuard guard(devs[q]);
@@ -1627,33 +1572,48 @@ int run_batch_multi(const fec_t* code, const uint8_t* coef, unsigned r, const gf
     std::vector<ShardResult> res(ndev);
     std::mutex mu;
     std::condition_variable cv;
-    size_t left = 0;
     // stripes [s0, s1) of shard d: balanced contiguous ranges (zfec_amd/shard.py shard_range)
     const size_t base = nstripes / ndev, extra = nstripes % ndev;
-    for (size_t d = 0; d < ndev; ++d) {
+    const size_t shards = std::min(ndev, nstripes);  // the non-empty ones: d < nstripes
+    size_t left = shards;  // shards not finished (or never posted); guarded by mu
+    // The workers reference this frame (mu, cv, left, res): whatever happens
+    // while posting (a thread that cannot be created, bad_alloc), the frame
+    // stays until every posted shard has finished.
+    int post_status = FEC_OK;
+    char post_msg[sizeof t_msg] = "";
+    for (size_t d = 0; d < shards; ++d) {
         const size_t s0 = d * base + std::min(d, extra), n = base + (d < extra ? 1 : 0);
-        if (n == 0) continue;
-        ++left;
         const gf* ps = src + s0 * sss;
         gf* pd = dst + s0 * dss;
         ShardResult* out = &res[d];
         const int dev = devices[d];
-        dev_worker(dev, d).post([=, &mu, &cv, &left] {
-            (void)hipSetDevice(dev);
-            const int st = guarded([&] {
-                return run_batch(code, coef, r, ps, sbs, sss, pd, dbs, dss, sz, n, nullptr,
-                                 (flags & ~FEC_FLAG_ASYNC) | FEC_FLAG_LIBRARY_STREAM);
+        const int pst = guarded([&] {
+            dev_worker(dev, d).post([=, &mu, &cv, &left] {
+                (void)hipSetDevice(dev);
+                const int st = guarded([&] {
+                    return run_batch(code, coef, r, ps, sbs, sss, pd, dbs, dss, sz, n, nullptr,
+                                     (flags & ~FEC_FLAG_ASYNC) | FEC_FLAG_LIBRARY_STREAM);
+                });
+                out->status = st;
+                if (st != FEC_OK) snprintf(out->msg, sizeof out->msg, "device %d: %s", dev, t_msg);
+                std::lock_guard<std::mutex> g(mu);
+                if (--left == 0) cv.notify_all();
             });
-            out->status = st;
-            if (st != FEC_OK) snprintf(out->msg, sizeof out->msg, "device %d: %s", dev, t_msg);
-            std::lock_guard<std::mutex> g(mu);
-            if (--left == 0) cv.notify_all();
+            return FEC_OK;
         });
+        if (pst != FEC_OK) {  // shards d.. were never posted: take them off the count
+            post_status = pst;
+            snprintf(post_msg, sizeof post_msg, "%s", t_msg);
+            std::lock_guard<std::mutex> g(mu);
+            left -= shards - d;
+            break;
+        }
     }
     {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return left == 0; });
     }
+    if (post_status != FEC_OK) return set_status(post_status, "%s", post_msg);
     for (const ShardResult& r0 : res)
         if (r0.status != FEC_OK) return set_status(r0.status, "%s", r0.msg);
     return set_status(FEC_OK);

@@ -36,20 +36,23 @@ namespace {
 // block of more than a few MiB is served by fresh pages (mmap, or a heap top
 // trimmed on free), so each call faults them in and each free unmaps them:
 // a 64 MiB K=3/M=10 encode from bytes ran at 2.6 GB/s that way against
-// 15.3 GB/s when freed blocks are reused.  The first call with
-// blocks of at least 1 MiB therefore lets glibc keep freed blocks for reuse:
-// M_MMAP_THRESHOLD 32 MiB (blocks under it come from the heap) and
-// M_TRIM_THRESHOLD 1 GiB (that much free heap is kept), as
-// zfec_amd.reuse_host_memory() does.  ZFEC_AMD_MALLOC=default keeps glibc's
-// policy.
+// 15.3 GB/s when freed blocks are reused.  Changing glibc's
+// policy is process-wide, and the reference module never does it, so it is
+// opt-in: with ZFEC_AMD_MALLOC=reuse in the environment the first call with
+// blocks of at least 1 MiB sets M_MMAP_THRESHOLD 32 MiB (blocks under it come
+// from the heap) and M_TRIM_THRESHOLD 1 GiB (that much free heap is kept), as
+// zfec_amd.reuse_host_memory() does.  By default nothing is changed.
+int g_mallopt_calls = 0;  // mallopt calls made by this module (_fec._mallopt_calls(), a test hook)
+
 void reuse_freed_outputs(Py_ssize_t sz) {
     static std::once_flag once;
     if (sz < (Py_ssize_t(1) << 20)) return;
     std::call_once(once, [] {
         const char* e = getenv("ZFEC_AMD_MALLOC");
-        if (e && !strcmp(e, "default")) return;
+        if (!e || strcmp(e, "reuse") != 0) return;
         (void)mallopt(M_MMAP_THRESHOLD, 32 << 20);
         (void)mallopt(M_TRIM_THRESHOLD, 1 << 30);
+        g_mallopt_calls += 2;
     });
 }
 
@@ -708,8 +711,11 @@ PyObject* py_batch_call(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
 
 PyObject* py_device_count(PyObject*, PyObject*) { return PyLong_FromLong(fec_device_count()); }
 PyObject* py_version(PyObject*, PyObject*) { return PyUnicode_FromString(fec_version()); }
+PyObject* py_mallopt_calls(PyObject*, PyObject*) { return PyLong_FromLong(g_mallopt_calls); }
 
 PyMethodDef module_functions[] = {
+    {"_mallopt_calls", py_mallopt_calls, METH_NOARGS,
+     "mallopt calls this module has made (0 unless ZFEC_AMD_MALLOC=reuse; a test hook)."},
     {"test_from_agl", test_from_agl, METH_NOARGS, "Encode/decode round trip of zfec's C self-test (on the GPU)."},
     {"device_count", py_device_count, METH_NOARGS, "Number of visible GPUs."},
     {"version", py_version, METH_NOARGS, "Library version."},

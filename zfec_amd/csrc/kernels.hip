@@ -1261,10 +1261,8 @@ const char* const kRowsNames[kRegK + 1][kRegR + 1] = {
     {"", "matapply_rows<4,1>", "matapply_rows<4,2>", "matapply_rows<4,3>", "matapply_rows<4,4>",
      "matapply_rows<4,5>", "matapply_rows<4,6>", "matapply_rows<4,7>", "matapply_rows<4,8>"}};
 
-// Output store policy of the register kernels (Config::store, ZFEC_HIP_STORE):
-// "nt" streams every store through the L2 write-back (nt); "ntsc1" writes
-// through the L2 at device scope (nt sc1); "auto" (default) takes nt sc1 for
-// single-stripe launches -- a few long rows, where it measured faster: the
+// Output store policy of the register kernels: nt sc1 (written through the L2
+// at device scope) for single-stripe launches -- a few long rows, where it measured faster: the
 // cfg2 64 MiB K=3/M=10 stripe, encode 68.5 -> 69.1-69.9 % of HBM from cold
 // caches, secondary decode 65.6 -> 68.0 %, bench value +1.2-1.5 % -- and nt for
 // batches of many stripes, where nt sc1 measured slower (256 x 1 MiB
@@ -1324,13 +1322,11 @@ hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
     const uint32_t grid = fill_regjob<K, R>(a, job, rows);
     if (!grid) return hipErrorInvalidValue;  // the caller splits
     void (*fn)(const RegJob<K, R>);
-    const StorePolicy sp = config().store;
     if (rows) {
         fn = matapply_rows<K, R, kArgLoad>;
         t_last_kernel = kRowsNames[K][R];
     } else {
-        fn = (sp == kStoreNtSc1 || (sp == kStoreAuto && a.nstripes == 1)) ? matapply_reg<K, R, 3, kPrefetch, kArgLoad>
-                                                                            : matapply_reg<K, R, 0, kPrefetch, kArgLoad>;
+        fn = a.nstripes == 1 ? matapply_reg<K, R, 3, kPrefetch, kArgLoad> : matapply_reg<K, R, 0, kPrefetch, kArgLoad>;
         t_last_kernel = kRegNames[K][R];
         if (sig && grid == 1) {  // one workgroup: it signals its own completion
             job.done_flag = sig;
@@ -1363,8 +1359,7 @@ hipError_t launch_pair(const ApplySpec& a, const ApplySpec& b, hipStream_t strea
     job.blocks_a = ga;
     job.pad_[0] = job.pad_[1] = job.pad_[2] = 0;
     // the register kernels' store policy, single-stripe (nt sc1) only when both are
-    const StorePolicy sp = config().store;
-    const bool sc1 = sp == kStoreNtSc1 || (sp == kStoreAuto && a.nstripes == 1 && b.nstripes == 1);
+    const bool sc1 = a.nstripes == 1 && b.nstripes == 1;
     void (*fn)(const PairJob<K, RA, RB>) = sc1 ? matapply_pair<K, RA, RB, 3> : matapply_pair<K, RA, RB, 0>;
     t_last_kernel = g_pair_names[K][RA][RB];
     return launch_job(reinterpret_cast<const void*>(fn), ga + gb, kBlock, 0, stream, job);
@@ -1583,10 +1578,11 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     // rows, and measured slower than half-idle CUs (profiles/r03_bsg_wgs.json:
     // 200/256 at RT 2 0.207 ms, RT 1 0.278 ms; 128/256 at RT 4 0.249 ms, RT 10
     // 0.351 ms, RT 2 0.312 ms).
+    constexpr uint32_t kBsgWgsPerCu = 4;
     const uint32_t need_rt = (r + 3) / 4;
     int ri = 0;
     while (ri + 1 < kBsgNumRT && kBsgRT[ri] < static_cast<int>(need_rt)) ++ri;
-    const uint64_t target = uint64_t(config().bsg_wgs_per_cu) * static_cast<uint64_t>(g_num_cu);
+    const uint64_t target = uint64_t(kBsgWgsPerCu) * static_cast<uint64_t>(g_num_cu);
     auto groups_of = [&](int i) { return (r + 4u * kBsgRT[i] - 1) / (4u * kBsgRT[i]); };
     while (ri > 1 && units * groups_of(ri) < target) --ri;
     const uint32_t ngroups = groups_of(ri);
@@ -1752,7 +1748,11 @@ hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev
     t_signal_flag = nullptr;  // an unconsumed launch_apply request must not outlive this launch
     t_signal_used = false;
     const uint32_t units = static_cast<uint32_t>(a.sz / 16);
-    const bool inl = host_in && host_sz <= a.sz && uint64_t(a.k) * units * 16 <= kOneInline;
+    // host_in: the caller has NOT copied the inputs anywhere the kernel can
+    // read; they must fit the argument block, or the launch is refused (no
+    // fallback to the bounce-buffer form, which would read stale memory)
+    const bool inl = host_in != nullptr;
+    if (inl && !one_inline_fits(a.k, a.sz, host_sz)) return hipErrorInvalidValue;
     thread_local OneJobInline big;  // ~5 KiB: not on the stack of every call
     OneJob& job = big.job;
     std::memset(&job, 0, sizeof job);

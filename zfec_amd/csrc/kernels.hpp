@@ -87,6 +87,13 @@ bool matapply_signal_used();
 // most 4,352 bytes) they are copied into the kernel's argument block and
 // a.in is not read.  hipErrorInvalidValue for other shapes.
 constexpr uint32_t kOneInlineBytes = 4352;  // inline input capacity of matapply_one's argument block
+// Whether k host inputs of host_sz bytes, padded to ksz (a whole number of
+// 16-byte units), go inside matapply_one's argument block: the one test both
+// run_single (which then skips the copy into the bounce buffer) and
+// launch_one use.
+constexpr bool one_inline_fits(uint32_t k, uint64_t ksz, uint64_t host_sz) {
+    return host_sz <= ksz && ksz % 16 == 0 && uint64_t(k) * ksz <= kOneInlineBytes;
+}
 hipError_t launch_one(const ApplySpec& a, hipStream_t stream, uint32_t* flag_dev, uint32_t seq,
                       const uint8_t* const* host_in = nullptr, uint64_t host_sz = 0);
 
