@@ -358,6 +358,89 @@ def test_c_abi_device_pointers_misaligned():
         assert int(out[:3].sum()) == 0 and int(out[3 + 7 * sz:].sum()) == 0  # no stray writes
 
 
+@pytest.mark.parametrize("k,m", [(3, 10), (1, 2), (4, 12), (2, 5)])
+def test_misaligned_outputs_aligned_store_path(k, m):
+    """Output rows at addresses that are not 16-byte multiples run the
+    register kernels' aligned-store form (matapply_reg<k,r,ma>: each lane
+    stores the aligned line made of its own tail and its neighbour's head,
+    wave ends and row ends byte-wise): bit-exact against the oracle for every
+    misalignment 1..15 of the packed rows' base, sizes around the 16-byte unit,
+    the 64-lane wave and the row end, encode and decode, with guard bytes on
+    both sides of the output buffer untouched."""
+    r = m - k
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(k * 100 + m)
+    st = torch.cuda.current_stream().cuda_stream
+    for sz in (1, 15, 16, 17, 1000, 1024, 1025, 64 * 16 * 2 + 9, 333334):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        expect = oracle.encode(k, m, data)
+        src = torch.from_numpy(data).cuda()
+        for d in ([1, 6, 15] if sz > 4096 else range(1, 16)):
+            out = torch.full((r * sz + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+            base = out.data_ptr() + 16 + d  # torch allocations are 256-byte aligned
+            code.encode_ptrs([src[j].data_ptr() for j in range(k)], [base + i * sz for i in range(r)],
+                             list(range(k, m)), sz, stream=st)
+            name = capi.last_kernel_name()
+            torch.cuda.synchronize()
+            host = out.cpu().numpy()
+            got = host[16 + d:16 + d + r * sz].reshape(r, sz)
+            assert (got == expect).all(), (k, m, sz, d, name)
+            assert (host[:16 + d] == 0xA5).all() and (host[16 + d + r * sz:] == 0xA5).all(), (sz, d)
+            if sz >= 64:
+                assert name == "matapply_reg<%d,%d,ma>" % (k, r), name
+        # decode into misaligned rows: every primary lost that the code can recover
+        nums = list(range(m - k, m)) if r >= k else list(range(r)) + list(range(k, m))[:k - r]
+        slots = place(sorted(nums), k)
+        allb = torch.from_numpy(np.concatenate([data, expect])).cuda()
+        missing = [i for i in range(k) if slots[i] != i]
+        rec = torch.full((len(missing) * sz + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        base = rec.data_ptr() + 16 + 9
+        code.decode_ptrs([allb[b].data_ptr() for b in slots], [base + i * sz for i in range(len(missing))], slots,
+                         sz, stream=st)
+        torch.cuda.synchronize()
+        host = rec.cpu().numpy()
+        assert (host[25:25 + len(missing) * sz].reshape(len(missing), sz) == data[missing]).all(), (k, m, sz)
+        assert (host[:25] == 0x5A).all() and (host[25 + len(missing) * sz:] == 0x5A).all()
+
+
+def test_misaligned_outputs_batches_and_headline_size():
+    """The aligned-store form in batches (outputs at a misaligned base with a
+    stripe stride that is a 16-byte multiple: the form applies; an odd stripe
+    stride: the plain form) and at the cfg2 size (64 MiB stripe, outputs at 6
+    mod 16; slices at the start, the middle and the end against the oracle)."""
+    k, m, r = 3, 10, 7
+    code = capi.Code(k, m)
+    rng = np.random.default_rng(606)
+    st = torch.cuda.current_stream().cuda_stream
+    for sz, ns, oss, kind in ((5000, 37, 7 * 5008, "ma"), (5000, 37, 7 * 5000 + 3, "plain")):
+        data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+        src = torch.from_numpy(data).cuda()
+        out = torch.full((ns * oss + 256,), 0xA5, dtype=torch.uint8, device="cuda")
+        base = out.data_ptr() + 16 + 6
+        code.encode_batch(src.data_ptr(), sz, k * sz, base, sz, oss, list(range(k, m)), sz, ns, stream=st)
+        name = capi.last_kernel_name()
+        torch.cuda.synchronize()
+        host = out.cpu().numpy()
+        assert name.endswith(",ma>") == (kind == "ma"), (kind, name)
+        assert (host[:22] == 0xA5).all()
+        for s in range(ns):
+            rows = np.stack([host[22 + s * oss + i * sz:][:sz] for i in range(r)])
+            assert (rows == oracle.encode(k, m, data[s])).all(), (kind, s)
+    sz = -(-(64 << 20) // 3)
+    src = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda")
+    out = torch.full((r * sz + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    base = out.data_ptr() + 16 + 6
+    code.encode_ptrs([src[j].data_ptr() for j in range(k)], [base + i * sz for i in range(r)], list(range(k, m)), sz,
+                     stream=st)
+    assert capi.last_kernel_name() == "matapply_reg<3,7,ma>"
+    torch.cuda.synchronize()
+    got = out[22:22 + r * sz].view(r, sz)
+    for a in (0, sz // 2 - 3000, sz - 6000):
+        sl = src[:, a:a + 6000].cpu().numpy()
+        assert (got[:, a:a + 6000].cpu().numpy() == oracle.encode(k, m, sl)).all(), a
+    assert int((out[:22] != 0xA5).sum()) == 0 and int((out[22 + r * sz:] != 0xA5).sum()) == 0
+
+
 @pytest.mark.parametrize("k,m,sz", [(3, 10, 100003), (10, 16, 65539), (20, 60, 4099)])
 def test_slab_split_equals_whole_stripe(k, m, sz):
     """One stripe split into byte-range slabs (zfec_amd.shard.slab_range, the
