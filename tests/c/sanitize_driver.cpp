@@ -160,7 +160,7 @@ void check_config_reload() {
         while (!stop) {
             const zfec_hip::Config& c = zfec_hip::config();
             CHECK(c.launch_units >= 1024);
-            CHECK(c.jit.max_tile >= 1);
+            CHECK(c.zc_limit > 0 && c.pack_limit > 0);
         }
     });
     w.join();

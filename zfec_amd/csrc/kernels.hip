@@ -187,73 +187,6 @@ __device__ inline void store_tail(uint8_t* p, u32x4 v, uint32_t nb) {
     for (uint32_t b = 0; b < nb; ++b) p[b] = static_cast<uint8_t>(w[b >> 2] >> (8 * (b & 3)));
 }
 
-// ---- outputs at addresses that are not 16-byte multiples ----------------------
-// A 16-byte store straddling two 16-byte lines costs bandwidth: a K=3/M=10
-// 64 MiB encode ran 5.4 TB/s with its outputs at 6 (mod 16) against 6.2
-// aligned, while misaligned loads cost nothing (tools/mb_encode.hip,
-// DESIGN.md §3).  So for an output row at d = address % 16 != 0, lane l (16
-// bytes of the row at block offset off) stores the ALIGNED 16 bytes at off +
-// h (h = 16 - d): its own last d bytes and the first h bytes of lane l+1's
-// unit, fetched with a DPP wave shift.  Lane 63, and units whose line would
-// run past the row's end, store their own tail bytes; lane 0, the row's first
-// unit and units whose previous line was not stored whole store their own
-// head bytes -- both with naturally aligned dword / byte stores.
-
-// (a ++ b)[h .. h + 16): the 16 bytes at byte offset h (0..15, wave-uniform)
-// of the 32-byte concatenation of a and b.
-__device__ __forceinline__ u32x4 funnel16(const u32x4& a, const u32x4& b, uint32_t h) {
-    const uint32_t s = h & 3u;
-    auto ab = [s](uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbyte(hi, lo, s); };
-    switch (h >> 2) {
-    case 0: return u32x4{ab(a.y, a.x), ab(a.z, a.y), ab(a.w, a.z), ab(b.x, a.w)};
-    case 1: return u32x4{ab(a.z, a.y), ab(a.w, a.z), ab(b.x, a.w), ab(b.y, b.x)};
-    case 2: return u32x4{ab(a.w, a.z), ab(b.x, a.w), ab(b.y, b.x), ab(b.z, b.y)};
-    default: return u32x4{ab(b.x, a.w), ab(b.y, b.x), ab(b.z, b.y), ab(b.w, b.z)};
-    }
-}
-
-// Bytes [lo, hi) of the 16-byte line v at the 16-byte aligned address p:
-// whole dwords as dword stores, the rest byte by byte.
-__device__ inline void store_line_bytes(uint8_t* p, const u32x4& v, uint32_t lo, uint32_t hi) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t b0 = 4 * q, b1 = b0 + 4;
-        if (hi <= b0 || lo >= b1) continue;
-        if (lo <= b0 && b1 <= hi) {
-            *reinterpret_cast<uint32_t*>(p + b0) = w[q];
-            continue;
-        }
-        for (uint32_t b = lo > b0 ? lo : b0; b < (hi < b1 ? hi : b1); ++b)
-            p[b] = static_cast<uint8_t>(w[q] >> (8 * (b - b0)));
-    }
-}
-
-// Store lane's 16 bytes y of row `rowp` (block offset off, row length sz;
-// the unit is whole when off + 16 <= sz) when rowp % 16 == d != 0.
-template <int SP>
-__device__ __forceinline__ void store_misaligned(uint8_t* rowp, uint32_t d, const u32x4& y, uint64_t off,
-                                                 uint64_t sz) {
-    const uint32_t h = 16u - d, lane = threadIdx.x & 63u;
-    u32x4 nx;  // lane l+1's bytes (DPP wave_shl:1)
-    nx.x = __builtin_amdgcn_update_dpp(0u, y.x, 0x130, 0xF, 0xF, false);
-    nx.y = __builtin_amdgcn_update_dpp(0u, y.y, 0x130, 0xF, 0xF, false);
-    nx.z = __builtin_amdgcn_update_dpp(0u, y.z, 0x130, 0xF, 0xF, false);
-    nx.w = __builtin_amdgcn_update_dpp(0u, y.w, 0x130, 0xF, 0xF, false);
-    // lane l+1 holds unit off + 16 of this row whenever that line ends inside the row
-    if (lane != 63u && off + h + 16 <= sz) {
-        store16_pol<SP>(rowp + off + h, funnel16(y, nx, h));
-    } else if (off + h < sz) {  // own tail: row bytes [off + h, min(off + 16, sz))
-        const uint64_t n = sz - off - h;
-        store_line_bytes(rowp + off + h, funnel16(y, y, h), 0, n < d ? static_cast<uint32_t>(n) : d);
-    }
-    // own head, row bytes [off, min(off + h, sz)), unless lane l-1 stored it in its line
-    if (lane == 0u || off == 0 || off + h > sz) {
-        const uint64_t n = sz - off;
-        store_line_bytes(rowp + off + h - 16, funnel16(y, y, h), d, d + (n < h ? static_cast<uint32_t>(n) : h));
-    }
-}
-
 // Walks this lane's (stripe, chunk) units in grid-stride order without a
 // division per step.  (An XCD-contiguous workgroup order measured 2 % slower
 // on 256 x 1 MiB K=3/M=10 encodes from cold caches, profiles/r02_mb_cold.log.)
@@ -342,13 +275,9 @@ __device__ __forceinline__ Tab reg_table(const RegJob<K, R>& job, uint32_t i) {
 
 // One (stripe, chunk) unit: load K x 16 bytes, store R x 16 bytes.  AL: each
 // row's tables and output pointer are loaded (scalar loads) right before use.
-// MA: rows whose output address is not a 16-byte multiple store aligned lines
-// (store_misaligned; the launch guarantees out_sstride % 16 == 0 or one
-// stripe, so a row's misalignment is the same in every stripe); `off` is the
-// unit's offset in its block.
-template <int K, int R, int SP, bool AL, bool MA, size_t OFF = 0>
+template <int K, int R, int SP, bool AL, size_t OFF = 0>
 __device__ __forceinline__ void reg_compute_store(const RegJob<K, R>& job, const Tab (&T)[R][K], const u32x4 (&x)[K],
-                                                  uint64_t ob, bool full, uint32_t nb, uint64_t off) {
+                                                  uint64_t ob, bool full, uint32_t nb) {
     Sel sel[4][K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -375,13 +304,6 @@ __device__ __forceinline__ void reg_compute_store(const RegJob<K, R>& job, const
             out = job.out[r];
         }
         const u32x4 y{gf_dot<K>(t, sel[0]), gf_dot<K>(t, sel[1]), gf_dot<K>(t, sel[2]), gf_dot<K>(t, sel[3])};
-        if constexpr (MA) {
-            const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out)) & 15u;  // wave-uniform
-            if (d != 0u) {
-                store_misaligned<SP>(out + (ob - off), d, y, off, job.sz);
-                continue;
-            }
-        }
         if (full)
             store16_pol<SP>(out + ob, y);
         else
@@ -407,7 +329,7 @@ __device__ __forceinline__ void reg_load(const RegJob<K, R>& job, u32x4 (&x)[K],
 // caches the 3-row decode is slower with it, profiles/r02_reg_pf_ab.log).
 // SP: output store policy (store16_pol).  AL: tables and output pointers read
 // where they are used (reg_compute_store).
-template <int K, int R, int SP, bool PF, bool AL, size_t OFF, bool MA = false>
+template <int K, int R, int SP, bool PF, bool AL, size_t OFF>
 __device__ __forceinline__ void reg_body(const RegJob<K, R>& job, uint32_t block) {
     Tab T[R][K];
     if constexpr (!AL) {
@@ -422,16 +344,16 @@ __device__ __forceinline__ void reg_body(const RegJob<K, R>& job, uint32_t block
     UnitIter u(job, block);
     if constexpr (PF) {
         u32x4 x[K];
-        Span sp = chunk_span<kChunk, !MA>(u.c, sz, nfull);
+        Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
         uint64_t ob = u.s * job.out_sstride + sp.off;
         if (u.s < job.nstripes) reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
         while (u.s < job.nstripes) {
             UnitIter v = u;
             v.next(job);
-            const Span spn = chunk_span<kChunk, !MA>(v.c, sz, nfull);
+            const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
             u32x4 xn[K];
             if (v.s < job.nstripes) reg_load<K, R>(job, xn, v.s * job.in_sstride + spn.off, spn.full, spn.nb);
-            reg_compute_store<K, R, SP, AL, MA, OFF>(job, T, x, ob, sp.full, sp.nb, sp.off);
+            reg_compute_store<K, R, SP, AL, OFF>(job, T, x, ob, sp.full, sp.nb);
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = xn[j];
             sp = spn;
@@ -440,19 +362,18 @@ __device__ __forceinline__ void reg_body(const RegJob<K, R>& job, uint32_t block
         }
     } else {
         while (u.s < job.nstripes) {
-            const Span sp = chunk_span<kChunk, !MA>(u.c, sz, nfull);
+            const Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
             u32x4 x[K];
             reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
-            reg_compute_store<K, R, SP, AL, MA, OFF>(job, T, x, u.s * job.out_sstride + sp.off, sp.full, sp.nb,
-                                                     sp.off);
+            reg_compute_store<K, R, SP, AL, OFF>(job, T, x, u.s * job.out_sstride + sp.off, sp.full, sp.nb);
             u.next(job);
         }
     }
 }
 
-template <int K, int R, int SP, bool PF, bool AL, bool MA = false>
+template <int K, int R, int SP, bool PF, bool AL>
 __global__ __launch_bounds__(kBlock) void matapply_reg(const RegJob<K, R> job) {
-    reg_body<K, R, SP, PF, AL, 0, MA>(job, blockIdx.x);
+    reg_body<K, R, SP, PF, AL, 0>(job, blockIdx.x);
     // one-workgroup launches of a synchronous small call: publish completion
     // in pinned host memory, so the host need not wait in
     // hipStreamSynchronize (fec_abi.cpp run_single).  Every storing wave waits
@@ -640,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void matapply_rows(const RegJob<K, R> job) 
         }
 #pragma unroll
         for (int h = 0; h < 4; ++h)
-            if (live[h]) reg_compute_store<K, R, 0, AL, false>(job, T, x[h], s * job.out_sstride + o[h], true, 16u, o[h]);
+            if (live[h]) reg_compute_store<K, R, 0, AL>(job, T, x[h], s * job.out_sstride + o[h], true, 16u);
     }
 }
 
@@ -1329,13 +1250,6 @@ const char* const kRegNames[kRegK + 1][kRegR + 1] = {
      "matapply_reg<3,6>", "matapply_reg<3,7>", "matapply_reg<3,8>"},
     {"", "matapply_reg<4,1>", "matapply_reg<4,2>", "matapply_reg<4,3>", "matapply_reg<4,4>", "matapply_reg<4,5>",
      "matapply_reg<4,6>", "matapply_reg<4,7>", "matapply_reg<4,8>"}};
-// the aligned-store form for outputs off 16-byte lines (store_misaligned)
-const char* const kRegMaNames[kRegK + 1][kRegR + 1] = {
-    {},
-    {"", "matapply_reg<1,1,ma>", "matapply_reg<1,2,ma>", "matapply_reg<1,3,ma>", "matapply_reg<1,4,ma>", "matapply_reg<1,5,ma>", "matapply_reg<1,6,ma>", "matapply_reg<1,7,ma>", "matapply_reg<1,8,ma>"},
-    {"", "matapply_reg<2,1,ma>", "matapply_reg<2,2,ma>", "matapply_reg<2,3,ma>", "matapply_reg<2,4,ma>", "matapply_reg<2,5,ma>", "matapply_reg<2,6,ma>", "matapply_reg<2,7,ma>", "matapply_reg<2,8,ma>"},
-    {"", "matapply_reg<3,1,ma>", "matapply_reg<3,2,ma>", "matapply_reg<3,3,ma>", "matapply_reg<3,4,ma>", "matapply_reg<3,5,ma>", "matapply_reg<3,6,ma>", "matapply_reg<3,7,ma>", "matapply_reg<3,8,ma>"},
-    {"", "matapply_reg<4,1,ma>", "matapply_reg<4,2,ma>", "matapply_reg<4,3,ma>", "matapply_reg<4,4,ma>", "matapply_reg<4,5,ma>", "matapply_reg<4,6,ma>", "matapply_reg<4,7,ma>", "matapply_reg<4,8,ma>"},};
 
 const char* const kRowsNames[kRegK + 1][kRegR + 1] = {
     {},
@@ -1413,17 +1327,19 @@ hipError_t launch_reg(const ApplySpec& a, hipStream_t stream, uint32_t* sig) {
         fn = matapply_rows<K, R, kArgLoad>;
         t_last_kernel = kRowsNames[K][R];
     } else {
-        // outputs off 16-byte lines: the aligned-store form, where a row's
-        // misalignment is the same in every stripe
+        // Single stripes store nt sc1 -- unless an output row starts off a
+        // 16-byte line: its 16-byte stores straddle two lines, and written
+        // through (sc1) each straddling store costs a partial-line write; nt
+        // alone lets the L2 merge the halves.  K=3/M=10 64 MiB, outputs at 6
+        // (mod 16): nt sc1 47.2 us, nt 41.6-42.0 us, aligned 39.6
+        // (tools/misaligned_bench.py, profiles/r04_misaligned_ab.json; staging
+        // the rows through LDS to store aligned lines measured 56-62 us, and
+        // assembling them across lanes with DPP 90 us).
         bool ma = false;
         for (int i = 0; i < R; ++i) ma = ma || (reinterpret_cast<uintptr_t>(a.out[i]) & 15u) != 0;
-        ma = ma && (a.nstripes == 1 || a.out_sstride % 16 == 0);
-        if (ma)
-            fn = a.nstripes == 1 ? matapply_reg<K, R, 3, kPrefetch, kArgLoad, true>
-                                 : matapply_reg<K, R, 0, kPrefetch, kArgLoad, true>;
-        else
-            fn = a.nstripes == 1 ? matapply_reg<K, R, 3, kPrefetch, kArgLoad> : matapply_reg<K, R, 0, kPrefetch, kArgLoad>;
-        t_last_kernel = ma ? kRegMaNames[K][R] : kRegNames[K][R];
+        fn = a.nstripes == 1 && !ma ? matapply_reg<K, R, 3, kPrefetch, kArgLoad>
+                                    : matapply_reg<K, R, 0, kPrefetch, kArgLoad>;
+        t_last_kernel = kRegNames[K][R];
         if (sig && grid == 1) {  // one workgroup: it signals its own completion
             job.done_flag = sig;
             job.done_seq = t_signal_seq;
