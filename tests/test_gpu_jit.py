@@ -164,3 +164,60 @@ def test_jit_off_uses_table_kernels():
         assert (par == oracle.encode(k, m, data.cpu().numpy())).all()
     finally:
         capi.jit_mode(prev)
+
+
+_REMOVED_KNOBS_CHILD = r"""
+import json, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch
+from zfec_amd import capi
+from oracle import oracle
+
+capi.jit_mode(capi.JIT_FORCE)
+k, m, sz, ns = 20, 60, 52429, 2
+r = m - k
+rng = np.random.default_rng(int(sys.argv[2]))
+data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+src = torch.from_numpy(data).cuda()
+par = torch.zeros((ns, r, sz), dtype=torch.uint8, device="cuda")
+code = capi.Code(k, m)
+code.encode_batch(src.data_ptr(), sz, k * sz, par.data_ptr(), sz, r * sz, list(range(k, m)), sz, ns)
+enc_kernel = capi.last_kernel_name()
+torch.cuda.synchronize()
+p = par.cpu().numpy()
+ok_enc = all((p[s] == oracle.encode(k, m, data[s])).all() for s in range(ns))
+slots = list(range(m - k, m))  # every primary lost
+recv = par[:, r - k:].contiguous()
+rec = torch.zeros((ns, k, sz), dtype=torch.uint8, device="cuda")
+code.decode_batch(recv.data_ptr(), sz, k * sz, rec.data_ptr(), sz, k * sz, slots, sz, ns)
+dec_kernel = capi.last_kernel_name()
+torch.cuda.synchronize()
+ok_dec = bool((rec.cpu().numpy() == data).all())
+print(json.dumps({"enc": enc_kernel, "dec": dec_kernel, "ok_enc": bool(ok_enc), "ok_dec": ok_dec}))
+"""
+
+
+@pytest.mark.parametrize("env", [{"ZFEC_HIP_JIT_PROBE": "1"}, {"ZFEC_HIP_JIT_PROBE": "2"},
+                                 {"ZFEC_HIP_JIT_TILE": "3", "ZFEC_HIP_JIT_ORDER": "1", "ZFEC_HIP_JIT_PREFETCH": "0",
+                                  "ZFEC_HIP_JIT_STORE": "17", "ZFEC_HIP_STORE": "nt", "ZFEC_HIP_BSG_WGS": "1"}])
+def test_removed_knobs_cannot_change_bytes(env):
+    """Round 3's measurement-only probe variants (ZFEC_HIP_JIT_PROBE=1 read
+    zeros, =2 wrote the XOR of the inputs) and the other variant knobs are
+    gone from the library: with them set, a forced-JIT K=20/M=60 encode and an
+    all-primaries-lost decode in a fresh process still match the oracle, on
+    the specialised kernels (zfec/fec.c:487-505, :527-557)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    e.update(env)
+    res = subprocess.run([sys.executable, "-c", _REMOVED_KNOBS_CHILD, root, str(len(env))], env=e,
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["ok_enc"] and out["ok_dec"], out
+    assert out["enc"].startswith("zfec_hip_bitslice_k20_r40") and out["dec"].startswith("zfec_hip_bitslice_k20_r20"), out

@@ -14,6 +14,10 @@
 //             workgroup, 10 rows each, after all 4 waves loaded the unit's
 //             inputs (the unit's input pieces read 4 times, mostly from L2)
 //   rows      one 16-byte unit per lane (a 1 KiB piece per wave per row)
+//   *_occ3    the same with 48 KiB of dynamic LDS per workgroup: at most 3
+//             workgroups (12 waves) per CU, the JIT kernel's residency (156
+//             VGPRs: 3 waves per SIMD) -- round 4: is the piece length or the
+//             residency what separates wave1k from the JIT kernel?
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mb_pattern.hip -o tools/mb_pattern.exe
 #include <hip/hip_runtime.h>
@@ -135,13 +139,13 @@ __global__ __launch_bounds__(256) void rows16(Set s) {
 
 typedef void (*Fn)(Set);
 
-float run(Fn fn, uint32_t grid, const std::vector<Set>& sets, int reps) {
+float run(Fn fn, uint32_t grid, const std::vector<Set>& sets, int reps, uint32_t lds = 0) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int i = 0; i < 4; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, 0, sets[i % sets.size()]);
+    for (int i = 0; i < 4; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, 0, sets[i % sets.size()]);
     CK(hipEventRecord(a, 0));
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, 0, sets[(i + 4) % sets.size()]);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, 0, sets[(i + 4) % sets.size()]);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     CK(hipGetLastError());
@@ -173,18 +177,23 @@ int main(int argc, char** argv) {
         const char* name;
         Fn fn;
         uint32_t grid;
+        uint32_t lds;
     };
     const V vs[] = {
-        {"wave1k", wave_unit<1024>, g_wave(1024)},   {"wave2k", wave_unit<2048>, g_wave(2048)},
-        {"wave4k", wave_unit<4096>, g_wave(4096)},   {"split1k", split_unit<1024>, g_split(1024)},
-        {"split2k", split_unit<2048>, g_split(2048)}, {"rows16", rows16, (kLd / 16 * kNs + 255) / 256},
+        {"wave1k", wave_unit<1024>, g_wave(1024), 0},   {"wave2k", wave_unit<2048>, g_wave(2048), 0},
+        {"wave4k", wave_unit<4096>, g_wave(4096), 0},   {"split1k", split_unit<1024>, g_split(1024), 0},
+        {"split2k", split_unit<2048>, g_split(2048), 0}, {"rows16", rows16, (kLd / 16 * kNs + 255) / 256, 0},
+        {"wave1k_occ3", wave_unit<1024>, g_wave(1024), 48u << 10},
+        {"wave2k_occ3", wave_unit<2048>, g_wave(2048), 48u << 10},
+        {"split1k_occ3", split_unit<1024>, g_split(1024), 48u << 10},
+        {"split2k_occ3", split_unit<2048>, g_split(2048), 48u << 10},
     };
     printf("K=20/M=60 pattern, %u stripes of %u-byte rows (row stride %u), 2 sets of %.2f GB, %d reps\n", kNs, kSz,
            kLd, (double(kNs) * (K + R) * kLd) / 1e9, reps);
     for (int round = 0; round < 3; ++round) {
         printf("-- round %d\n", round);
         for (const V& v : vs) {
-            const float ms = run(v.fn, v.grid, sets, reps);
+            const float ms = run(v.fn, v.grid, sets, reps, v.lds);
             printf("%-8s %8.1f us  %7.1f GB/s  (%.3f of 8 TB/s)  grid %u\n", v.name, ms * 1e3,
                    bytes / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 8e12, v.grid);
             fflush(stdout);

@@ -51,7 +51,8 @@ def trace_means(path):
 
 
 def short(n):
-    return n.replace("void zfec_hip::(anonymous namespace)::", "").split("(")[0]
+    n = n.replace("void ", "").replace("zfec_hip::(anonymous namespace)::", "").replace("zfec_hip::", "")
+    return n.split("(")[0]
 
 
 def main():
