@@ -16,7 +16,7 @@ LIB      := zfec_amd/libzfec_hip.so
 PYEXT    := zfec_amd/_fec$(EXT)
 # every object depends on every header: config.hpp embeds bitslice.hpp's options, so a
 # header change must rebuild all of them (a stale object reads a stale Config layout)
-HDRS     := $(wildcard $(SRC)/*.hpp) include/zfec_hip.h
+HDRS     := $(wildcard $(SRC)/*.hpp) $(SRC)/gf_routines.inc include/zfec_hip.h
 HIPFLAGS := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function
 
 all: $(LIB) $(PYEXT) oracle

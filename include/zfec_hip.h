@@ -243,11 +243,13 @@ int fec_jit_mode(int mode);
 
 /* Wide-code launches that no compiled specialised kernel serves (a decode of
  * an erasure pattern seen for the first time, small launches, JIT off) run on
- * matapply_bsg: the same bit-sliced arithmetic with the coefficient matrix as
- * run-time data (no compile step).  mode 1 = on (default; environment
- * ZFEC_HIP_GENERIC=0 starts it off), 0 = off (the table-lookup kernels
- * serve them).  Returns the previous mode; any other value only queries.
- * Results are bit-identical either way. */
+ * the bit-sliced kernels that take the coefficient matrix as run-time data (no
+ * compile step): mode 2 = matapply_bsr where it fits (k <= 32, r <= 40; the
+ * specialised kernels' instruction stream, one call per coefficient), else
+ * matapply_bsg (default); 1 = matapply_bsg only; 0 = off (the table-lookup
+ * kernels serve them; environment ZFEC_HIP_GENERIC=0 / 1 starts in mode 0 /
+ * 1).  Returns the previous mode; any other value only queries.  Results are
+ * bit-identical in every mode. */
 int fec_generic_mode(int mode);
 
 /* Wait for background compiles; returns the number of compiled kernels. */

@@ -1,0 +1,75 @@
+"""CPU checks of zfec_amd/csrc/gf_routines.inc, the multiply-by-constant
+routines matapply_bsr calls (one per coefficient):
+
+- the file is what tools/gen_gf_routines.py writes (no hand edits, no stale copy);
+- every routine, executed by a small interpreter of its v_bitop3_b32 lines on
+  bit-planes of random bytes -- after the combination XORs that bsr_input emits
+  -- adds exactly c * x (the oracle's gf_mul, zfec/fec.c:58-86 via
+  oracle/fec_oracle.c) to the accumulator row;
+- every routine fits its 72-byte slot (the .org directives would fail the
+  build otherwise; this names the routine)."""
+
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "zfec_amd", "csrc", "gf_routines.inc")
+
+
+def test_generated_file_is_current():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_gf_routines.py"), "--check"])
+    assert r.returncode == 0, "gf_routines.inc differs from tools/gen_gf_routines.py output"
+
+
+def _parse():
+    text = open(INC).read()
+    body = text[text.index('"zfec_gf_routines:\\n"'):text.index('"zfec_gf_routines_end:')]
+    routines = {}
+    for m in re.finditer(r'"\.org zfec_gf_routines \+ (\d+)\\n"\s*\n\s*"([^"]*)"', body):
+        routines[int(m.group(1))] = m.group(2).split("\\n")
+    combos = re.search(r"bsr_input<1>.*?asm volatile\((.*?)s_getpc", text, re.S).group(1)
+    xors = re.findall(r"v_xor_b32 v(\d+), v(\d+), v(\d+)", combos)
+    return routines, [(int(a), int(b), int(c)) for a, b, c in xors]
+
+
+def _planes(x):
+    """32 bytes -> 8 bit-planes (plane b: bit t = bit b of byte t)."""
+    return [int(sum(((int(x[t]) >> b) & 1) << t for t in range(32))) for b in range(8)]
+
+
+def test_every_routine_multiplies():
+    routines, xors = _parse()
+    assert len(routines) == 256 and len(xors) == 22
+    rng = np.random.default_rng(72)
+    mul = np.array([[oracle.gf_mul(a, b) for b in range(256)] for a in range(256)], dtype=np.uint8)
+    op = re.compile(r"v_bitop3_b32 v(\d+), v(\d+), (v\d+|0), (v\d+|0) bitop3:0x96")
+    for c in range(256):
+        lines = routines[72 * c]
+        assert lines[-2] == "s_setpc_b64 s[30:31]" and lines[-1] == "", (c, lines[-2:])
+        body = lines[:-2]
+        assert 8 * len(body) + 4 <= 72, c
+        for trial in range(3):
+            x = rng.integers(0, 256, size=32, dtype=np.uint8)
+            acc0 = rng.integers(0, 256, size=32, dtype=np.uint8)
+            v = {}
+            for b, pl in enumerate(_planes(x)):
+                v[104 + b] = pl
+            for d, a, b in xors:
+                v[d] = v[a] ^ v[b]
+            for b, pl in enumerate(_planes(acc0)):
+                v[24 + b] = pl
+            for ln in body:
+                m = op.fullmatch(ln)
+                assert m, (c, ln)
+                d, s0, s1, s2 = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)
+                assert d == s0 and 24 <= d < 32, (c, ln)
+                val = lambda s: 0 if s == "0" else v[int(s[1:])]
+                v[d] = v[s0] ^ val(s1) ^ val(s2)
+            want = _planes(acc0 ^ mul[c][x])
+            assert [v[24 + b] for b in range(8)] == want, (c, trial)

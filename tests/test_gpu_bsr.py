@@ -1,0 +1,202 @@
+"""GPU parity of matapply_bsr (zfec_amd/csrc/kernels.hip, routines in
+gf_routines.inc): the run-time-data bit-sliced kernel that calls one
+precompiled multiply-by-constant routine per coefficient.  It serves launches
+of k <= 32 inputs and r <= 40 rows that no compiled JIT kernel serves -- above
+all decodes of an erasure pattern seen for the first time (zfec/fec.c:527-557
+decodes every pattern with one code path).  Bit-exact against the CPU oracle
+for every rows-per-wave instantiation (RT = 1..10) and wave count (1..4 row
+tiles), block sizes around the 2 KiB unit and its overlapping last unit,
+batched strided stripes at misaligned bases with guard bytes, random erasure
+patterns, and against matapply_bsg (generic mode 1) on the same launch."""
+
+import numpy as np
+import pytest
+
+import zfec_amd
+from zfec_amd import capi
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if zfec_amd.device_count() < 1:
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+
+
+@pytest.fixture
+def bsr_only(knobs):
+    """JIT off, generic mode 2 (matapply_bsr first), matapply_small off."""
+    prev_j, prev_g = capi.jit_mode(capi.JIT_OFF), capi.generic_mode(2)
+    knobs(ZFEC_HIP_SMALL_LANES=0)
+    yield
+    capi.jit_mode(prev_j)
+    capi.generic_mode(prev_g)
+
+
+def place(nums, k):
+    slots = [None] * k
+    sec = iter([n for n in nums if n >= k])
+    for n in nums:
+        if n < k:
+            slots[n] = n
+    return [s if s is not None else next(sec) for s in slots]
+
+
+def bsr_name(r):
+    nw = (r + 9) // 10
+    return "matapply_bsr<%d>" % (-(-r // nw))
+
+
+def is_bsr(name, r):
+    """matapply_bsr<RT> for r rows (RT = rows per wave), any variant suffix."""
+    want = bsr_name(r)[:-1]
+    return name.startswith(want) and name[len(want)] in ">,"
+
+
+# (k, m): r = m - k = 1..10 (one wave, RT = r), 13 / 20 (two waves), 25 (three), 31 / 40 (four)
+SHAPES = [(30, 31), (12, 14), (10, 13), (7, 11), (6, 11), (10, 16), (5, 12), (20, 28), (3, 12), (32, 42),
+          (20, 33), (12, 32), (16, 41), (2, 33), (20, 60), (32, 72)]
+
+
+@pytest.mark.parametrize("k,m", SHAPES)
+def test_bsr_encode_decode_vs_oracle(bsr_only, k, m):
+    rng = np.random.default_rng(k * 100 + m)
+    for sz in (2048, 2049, 4097, 9000):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        assert is_bsr(capi.last_kernel_name(), m - k), (capi.last_kernel_name(), k, m)
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        if all(n < k for n in nums):
+            nums = list(range(m - k, m))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz, nums)
+
+
+@pytest.mark.parametrize("k,m,sz,ns", [(10, 16, 5000, 9), (20, 60, 52429, 7), (6, 13, 2048, 33), (32, 40, 12345, 3),
+                                       (20, 33, 2100, 50)])
+def test_bsr_batched_strided_misaligned(bsr_only, k, m, sz, ns):
+    """Batched stripes at odd strides and misaligned bases: every stripe
+    against the oracle; bytes between rows and after the last one stay 0xA5."""
+    r = m - k
+    rng = np.random.default_rng(sz + ns)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    ld = sz + 24
+    base_in, base_out = 3, 5
+    src = torch.zeros(base_in + ns * k * ld, dtype=torch.uint8, device="cuda")
+    view = src[base_in:].view(ns, k, ld)
+    view[:, :, :sz] = torch.from_numpy(data).cuda()
+    dst = torch.full((base_out + ns * r * ld + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(src.data_ptr() + base_in, ld, k * ld, dst.data_ptr() + base_out, ld, r * ld,
+                      list(range(k, m)), sz, ns, stream=st)
+    torch.cuda.synchronize()
+    assert is_bsr(capi.last_kernel_name(), r), capi.last_kernel_name()
+    d = dst.cpu().numpy()
+    assert (d[:base_out] == 0xA5).all() and (d[base_out + ns * r * ld:] == 0xA5).all()
+    out = d[base_out:base_out + ns * r * ld].reshape(ns, r, ld)
+    assert (out[:, :, sz:] == 0xA5).all(), "write past a row"
+    for s in range(ns):
+        assert (out[s, :, :sz] == oracle.encode(k, m, data[s])).all(), s
+
+
+def test_bsr_fresh_erasure_patterns(bsr_only):
+    """cfg4's code, 20 random erasure patterns, each decoded once: recovered
+    blocks equal the inputs and the oracle."""
+    k, m, sz, ns = 20, 60, 52429, 16
+    ld = (sz + 255) // 256 * 256
+    g = torch.Generator(device="cuda").manual_seed(20)
+    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=g)
+    par = torch.zeros((ns, m - k, ld), dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, (m - k) * ld, list(range(k, m)), sz, ns,
+                      stream=st)
+    allb = torch.cat([data, par], dim=1)
+    rng = np.random.default_rng(61)
+    for p in range(20):
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        sl = place(nums, k)
+        miss = [i for i in range(k) if sl[i] >= k]
+        if not miss:
+            continue
+        rv = allb[:, sl, :].contiguous()
+        rec = torch.zeros((ns, len(miss), ld), dtype=torch.uint8, device="cuda")
+        code.decode_batch(rv.data_ptr(), ld, k * ld, rec.data_ptr(), ld, len(miss) * ld, sl, sz, ns, stream=st)
+        torch.cuda.synchronize()
+        if len(miss) * k >= 24:
+            assert is_bsr(capi.last_kernel_name(), len(miss)), capi.last_kernel_name()
+        assert bool(torch.equal(rec[:, :, :sz], data[:, miss, :sz])), nums
+        s = int(rng.integers(0, ns))
+        want = oracle.decode(k, m, rv[s, :, :sz].cpu().numpy(), sl)
+        assert (rec[s, :, :sz].cpu().numpy() == want).all(), nums
+
+
+def test_bsr_every_coefficient(bsr_only):
+    """Every routine: the 32/72 encode (253 of the 255 nonzero coefficients;
+    routine 0 runs for the padding rows of a tile) and decodes chosen until
+    their matrices have used the remaining ones, each against the oracle."""
+    k, m, sz = 32, 72, 4096
+    rng = np.random.default_rng(256)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    enc = zfec_amd.Encoder(k, m).encode(ins)
+    torch.cuda.synchronize()
+    assert is_bsr(capi.last_kernel_name(), m - k), capi.last_kernel_name()
+    assert (torch.stack(enc[k:]).cpu().numpy() == oracle.encode(k, m, data)).all()
+    cov = set(np.asarray(oracle.enc_matrix(k, m)).reshape(m, k)[k:].flatten().tolist())
+    dec = zfec_amd.Decoder(k, m)
+    tries = 0
+    while not cov >= set(range(1, 256)) and tries < 400:
+        tries += 1
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        sl = place(nums, k)
+        miss = [i for i in range(k) if sl[i] >= k]
+        if len(miss) * k < 24:
+            continue
+        dm = np.asarray(oracle.decode_matrix(k, m, sl)).reshape(k, k)
+        new = set(dm[miss].flatten().tolist()) - cov
+        if not new:
+            continue
+        cov |= new
+        got = dec.decode([enc[n] for n in nums], nums)
+        torch.cuda.synchronize()
+        assert is_bsr(capi.last_kernel_name(), len(miss)), capi.last_kernel_name()
+        assert (torch.stack(got).cpu().numpy() == data).all(), nums
+    assert cov >= set(range(1, 256)), sorted(set(range(1, 256)) - cov)
+
+
+@pytest.mark.parametrize("k,m", [(20, 60), (10, 16), (32, 42)])
+def test_bsr_equals_bsg(k, m):
+    """The same encode and fresh decode with generic mode 2 (matapply_bsr) and 1
+    (matapply_bsg): identical bytes."""
+    rng = np.random.default_rng(k + m)
+    sz = 70000
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+    prev_j = capi.jit_mode(capi.JIT_OFF)
+    res = {}
+    try:
+        for gen in (2, 1):
+            prev = capi.generic_mode(gen)
+            try:
+                enc = zfec_amd.Encoder(k, m).encode(ins)
+                torch.cuda.synchronize()
+                assert capi.last_kernel_name().startswith("matapply_bsr" if gen == 2 else "matapply_bsg")
+                dec = zfec_amd.Decoder(k, m).decode([enc[n] for n in nums], nums)
+                res[gen] = (torch.stack(enc[k:]).cpu(), torch.stack(dec).cpu())
+            finally:
+                capi.generic_mode(prev)
+    finally:
+        capi.jit_mode(prev_j)
+    assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
+    assert (res[2][1].numpy() == data).all()

@@ -42,7 +42,7 @@ def main():
                       stream=st.cuda_stream)
     torch.cuda.synchronize()
     res = bench.decode_fresh(code, k, m, sz, ns, ld, data, par, recv, args.patterns, st)
-    res.update({"shape": args.shape, "tag": args.tag, "env_x": os.environ.get("ZFEC_HIP_BSG_W")})
+    res.update({"shape": args.shape, "tag": args.tag, "generic": os.environ.get("ZFEC_HIP_GENERIC", "2")})
     print(json.dumps(res), flush=True)
 
 

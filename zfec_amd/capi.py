@@ -127,8 +127,9 @@ def jit_mode(mode=-1):
 
 
 def generic_mode(mode=-1):
-    """matapply_bsg (run-time-data bit-sliced kernel) on (1) / off (0) for
-    wide-code launches no JIT kernel serves; returns the previous mode."""
+    """Run-time-data bit-sliced kernels for wide-code launches no JIT kernel
+    serves: 2 = matapply_bsr where it fits, else matapply_bsg (default);
+    1 = matapply_bsg only; 0 = off (table kernels).  Returns the previous mode."""
     return lib().fec_generic_mode(mode)
 
 

@@ -1153,7 +1153,7 @@ FEC_API int fec_jit_mode(int mode) {
 
 FEC_API int fec_generic_mode(int mode) {
     const int prev = generic_mode();
-    if (mode == 0 || mode == 1) set_generic_mode(mode);
+    if (mode >= 0 && mode <= 2) set_generic_mode(mode);
     set_status(FEC_OK);
     return prev;
 }

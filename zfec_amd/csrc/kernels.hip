@@ -1104,6 +1104,189 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 }
 
 // ---------------------------------------------------------------------------
+// matapply_bsr<RT>: bit-sliced with the coefficients as run-time data, at the
+// instruction count of a specialised (JIT) kernel.  Multiplying the 32 bytes
+// of a lane by c and adding them to an accumulator row is, on bit-planes, eight
+// XOR3s whose operands depend on c only; gf_routines.inc holds those eight
+// instructions for every c as a routine (zfec_gf_routines + 72 c) working on
+// fixed registers: the input's combinations of planes (built once per input
+// per wave) and accumulator row 0, offset to row rr by VGPR index mode.  A
+// coefficient costs a call (five scalar instructions and two jumps, no LDS
+// read) instead of matapply_bsg's sixteen LDS reads or a compile per matrix.
+//
+// Workgroup = one unit (2 KiB of every block of a stripe, 32 bytes per lane,
+// like the JIT kernels) and nw waves, one per row tile of <= RT rows: the waves
+// first load, transpose and park the unit's k inputs as bit-planes in LDS
+// (k * 2 KiB, each wave a k / nw share), then each walks all k inputs for its
+// tile.  Coefficients: MatJob::coef as [wave][input][RTP] bytes (RTP = RT
+// rounded up to 4, rows past the tile 0: routine 0 only returns).
+// ---------------------------------------------------------------------------
+#include "gf_routines.inc"
+
+constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
+constexpr int kBsrBatch = 8;          // inputs a wave loads at once
+
+template <int RT>
+__host__ __device__ constexpr uint32_t bsr_rtp() {
+    return (RT + 3) / 4 * 4;
+}
+
+template <int RT>
+__global__ __launch_bounds__(256) void matapply_bsr(const MatJob job) {
+    constexpr uint32_t RTP = bsr_rtp<RT>();
+    extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = blockDim.x >> 6;
+    const uint32_t k = job.k, r = job.r;
+    const uint32_t kp = job.pad_ ? job.pad_ : k;  // inputs per LDS phase
+    const uint32_t r0 = wave * r / nw, rows = (wave + 1) * r / nw - r0;
+    const KPtr<MatJob> kj = kernarg_job<MatJob>();
+    const KWords cw = (KWords)kj->coef + wave * k * (RTP / 4);
+    const uint64_t sz = job.sz;
+    uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
+    while (s < job.nstripes) {
+        uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
+        if (off > sz - kBsrChunk) off = sz - kBsrChunk;  // the last unit ends at sz (overlapping its neighbour)
+        const uint64_t ib = s * job.in_sstride + off + lane * 16u;
+        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        uint32_t acc[RT][8];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
+        for (uint32_t ph = 0; ph < k; ph += kp) {
+            const uint32_t kn = k - ph < kp ? k - ph : kp;
+            // inputs -> bit-planes -> LDS, inputs wave, wave + nw, ... in batches
+            for (uint32_t j0 = wave; j0 < kn; j0 += kBsrBatch * nw) {
+                u32x4 x[kBsrBatch][2];
+#pragma unroll
+                for (int q = 0; q < kBsrBatch; ++q) {
+                    const uint32_t j = j0 + q * nw;
+                    if (j < kn) {  // wave-uniform
+                        const uint8_t* ip = kj->in[ph + j] + ib;
+                        x[q][0] = load16(ip);
+                        x[q][1] = load16(ip + 1024);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < kBsrBatch; ++q) {
+                    const uint32_t j = j0 + q * nw;
+                    if (j < kn) {
+                        uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
+                                         x[q][1].x, x[q][1].y, x[q][1].z, x[q][1].w};
+                        transpose8(v);
+                        bsr_planes[j * 128u + lane] = u32x4{v[0], v[1], v[2], v[3]};
+                        bsr_planes[j * 128u + 64u + lane] = u32x4{v[4], v[5], v[6], v[7]};
+                    }
+                }
+            }
+            __syncthreads();
+            // input j's planes and coefficient words are read during input j - 1
+            // (one wait drains LDS and scalar loads alike)
+            u32x4 pa = bsr_planes[lane], pb = bsr_planes[64u + lane];
+            uint32_t cwd[RTP / 4];
+#pragma unroll
+            for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[ph * (RTP / 4) + d];
+            for (uint32_t j = 0; j < kn; ++j) {
+                const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+                uint32_t offs[RT];
+#pragma unroll
+                for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
+                if (j + 1 < kn) {
+                    pa = bsr_planes[(j + 1) * 128u + lane];
+                    pb = bsr_planes[(j + 1) * 128u + 64u + lane];
+#pragma unroll
+                    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(ph + j + 1) * (RTP / 4) + d];
+                }
+                bsr_input<RT>(acc, p, offs);
+            }
+            __syncthreads();  // every wave has read the planes before they are overwritten
+        }
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            if (static_cast<uint32_t>(rr) < rows) {  // wave-uniform
+                transpose8(acc[rr]);
+                uint8_t* op = kj->out[r0 + rr] + ob;
+                store16_out<true>(op, u32x4{acc[rr][0], acc[rr][1], acc[rr][2], acc[rr][3]});
+                store16_out<true>(op + 1024, u32x4{acc[rr][4], acc[rr][5], acc[rr][6], acc[rr][7]});
+            }
+        }
+        c += job.gs_c;
+        s += job.gs_s;
+        if (c >= job.cps) {
+            c -= job.cps;
+            ++s;
+        }
+    }
+}
+
+// One wave per (unit, row tile), no LDS: the wave loads and transposes every
+// input of its unit itself (tiles of one unit are adjacent workgroups, so the
+// second tile's loads hit L2), two inputs in flight ahead.
+template <int RT>
+__global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
+    constexpr uint32_t RTP = bsr_rtp<RT>();
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = job.k, r = job.r, nt = job.pad_;
+    const KPtr<MatJob> kj = kernarg_job<MatJob>();
+    const uint64_t sz = job.sz;
+    const uint64_t total = uint64_t(job.nstripes) * job.cps * nt;
+    for (uint64_t v = blockIdx.x; v < total; v += gridDim.x) {
+        const uint32_t t = static_cast<uint32_t>(v % nt);
+        const uint64_t u = v / nt;
+        const uint32_t s = static_cast<uint32_t>(u / job.cps), c = static_cast<uint32_t>(u % job.cps);
+        const uint32_t r0 = t * r / nt, rows = (t + 1) * r / nt - r0;
+        const KWords cw = (KWords)kj->coef + t * k * (RTP / 4);
+        uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
+        if (off > sz - kBsrChunk) off = sz - kBsrChunk;
+        const uint64_t ib = s * job.in_sstride + off + lane * 16u;
+        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        uint32_t acc[RT][8];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr)
+#pragma unroll
+            for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
+        u32x4 a0 = load16(kj->in[0] + ib), a1 = load16(kj->in[0] + ib + 1024);
+        u32x4 b0 = a0, b1 = a1;
+        if (k > 1) {
+            b0 = load16(kj->in[1] + ib);
+            b1 = load16(kj->in[1] + ib + 1024);
+        }
+        uint32_t cwd[RTP / 4];
+#pragma unroll
+        for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[d];
+        for (uint32_t j = 0; j < k; ++j) {
+            uint32_t p[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            a0 = b0;
+            a1 = b1;
+            if (j + 2 < k) {
+                b0 = load16(kj->in[j + 2] + ib);
+                b1 = load16(kj->in[j + 2] + ib + 1024);
+            }
+            transpose8(p);
+            uint32_t offs[RT];
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
+            if (j + 1 < k) {
+#pragma unroll
+                for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(j + 1) * (RTP / 4) + d];
+            }
+            bsr_input<RT>(acc, p, offs);
+        }
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            if (static_cast<uint32_t>(rr) < rows) {
+                transpose8(acc[rr]);
+                uint8_t* op = kj->out[r0 + rr] + ob;
+                store16_out<true>(op, u32x4{acc[rr][0], acc[rr][1], acc[rr][2], acc[rr][3]});
+                store16_out<true>(op + 1024, u32x4{acc[rr][4], acc[rr][5], acc[rr][6], acc[rr][7]});
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // matapply_small: launches too small to fill the chip with the unit kernels,
 // for codes beyond the register kernels (k > 4 or r > 8).  The unit kernels
 // give each lane every output row of its slice: a K=20/M=60 stripe of 4 KiB
@@ -1668,20 +1851,98 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     return hipSuccess;
 }
 
+// ---- matapply_bsr dispatch ------------------------------------------------------
+// nw = ceil(r / 10) waves, one per row tile of <= RT = ceil(r / nw) rows.
+struct BsrVariant {
+    const void* fn = nullptr;
+    const void* fn_solo = nullptr;
+    char name[24] = "";
+    char name_solo[32] = "";
+};
+BsrVariant g_bsr_var[kBsrMaxRows + 1];
+std::once_flag g_bsr_once;
+
+template <int RT>
+void fill_bsr() {
+    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT>);
+    snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d>", RT);
+    g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
+    snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d,solo>", RT);
+    if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
+}
+
+void bsr_tiles(uint32_t r, uint32_t* nw, uint32_t* rt) {
+    *nw = (r + kBsrMaxRows - 1) / kBsrMaxRows;
+    *rt = (r + *nw - 1) / *nw;
+}
+
+bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    if (generic_mode() != 2 || k < 1 || k > static_cast<uint32_t>(kMaxIn) || r < 1 ||
+        r > 4u * kBsrMaxRows || sz < kBsrChunk || k * r < 24 || (k <= 4 && r <= 8))
+        return false;
+    uint32_t nw, rt;
+    bsr_tiles(r, &nw, &rt);
+    return nw * k * ((rt + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
+}
+
+hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
+    std::call_once(g_bsr_once, [] { fill_bsr<1>(); });
+    const uint32_t k = a.k, r = a.r;
+    uint32_t nw, rt;
+    bsr_tiles(r, &nw, &rt);
+    const uint32_t rtp = (rt + 3) / 4 * 4;
+    const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
+    const uint64_t units = cps * a.nstripes;
+    if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
+    MatJob job;
+    fill_matjob(a, job);
+    std::memset(job.coef, 0, size_t(nw) * k * rtp);
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t r0 = w * r / nw, rows = (w + 1) * r / nw - r0;
+        for (uint32_t j = 0; j < k; ++j)
+            for (uint32_t rr = 0; rr < rows; ++rr)
+                job.coef[(w * k + j) * rtp + rr] = a.coef[size_t(r0 + rr) * a.coef_stride + j];
+    }
+    const uint64_t cap = uint64_t(g_num_cu) * 32;
+    const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_s = static_cast<uint32_t>(grid / cps);
+    job.gs_c = static_cast<uint32_t>(grid % cps);
+    static const uint32_t kp_env = [] {
+        const char* e = getenv("ZFEC_HIP_BSR_KP");
+        return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+    }();
+    static const bool solo = [] {
+        const char* e = getenv("ZFEC_HIP_BSR_SOLO");
+        return e && e[0] == '1';
+    }();
+    if (solo) {
+        job.pad_ = nw;
+        const uint64_t vu = units * nw;
+        const uint64_t capw = uint64_t(g_num_cu) * 64;
+        t_last_kernel = g_bsr_var[rt].name_solo;
+        return launch_job(g_bsr_var[rt].fn_solo, static_cast<uint32_t>(vu < capw ? vu : capw), 64, 0, stream, job);
+    }
+    const uint32_t kp = kp_env && kp_env < k ? kp_env : k;
+    job.pad_ = kp;
+    t_last_kernel = g_bsr_var[rt].name;
+    return launch_job(g_bsr_var[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job);
+}
+
 }  // namespace
 
 int generic_mode() {
     int g = g_generic.load();
     if (g < 0) {
         const char* e = getenv("ZFEC_HIP_GENERIC");
-        g = (e && e[0] == '0') ? 0 : 1;
+        g = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
         int expect = -1;
         if (!g_generic.compare_exchange_strong(expect, g)) g = expect;  // set_generic_mode won the race
     }
     return g;
 }
 
-void set_generic_mode(int on) { g_generic.store(on ? 1 : 0); }
+void set_generic_mode(int mode) { g_generic.store(mode < 0 ? 0 : mode > 2 ? 2 : mode); }
 
 const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate) {
     if (!accumulate && k >= 1 && k <= static_cast<uint32_t>(kRegK) && r >= 1 && r <= static_cast<uint32_t>(kRegR))
@@ -1744,6 +2005,7 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
             return se;
         }
     }
+    if (!a.accumulate && bsr_shape_ok(k, r, a.sz)) return launch_bsr(a, stream);
     if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);

@@ -106,10 +106,12 @@ const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
 // bitslice.hpp).
 const char* matapply_last_kernel();
 
-// matapply_bsg (bit-sliced, coefficients as run-time data) for wide-code
-// launches that no specialised JIT kernel serves: 1 = on (default; env
-// ZFEC_HIP_GENERIC=0 starts it off), 0 = off (the table kernels serve).
+// The bit-sliced kernels with the coefficients as run-time data, for wide-code
+// launches that no specialised JIT kernel serves: 2 = matapply_bsr where its
+// shape fits (k <= 32, r <= 40), else matapply_bsg (default); 1 = matapply_bsg
+// only; 0 = off (the table kernels serve).  Env ZFEC_HIP_GENERIC=0/1 starts
+// in mode 0/1.
 int generic_mode();
-void set_generic_mode(int on);
+void set_generic_mode(int mode);
 
 }  // namespace zfec_hip
