@@ -247,8 +247,8 @@ int fec_jit_mode(int mode);
  * compile step): mode 2 = matapply_bsr where it fits (k <= 32, r <= 40; the
  * specialised kernels' instruction stream, one call per coefficient), else
  * matapply_bsg (default); 1 = matapply_bsg only; 0 = off (the table-lookup
- * kernels serve them; environment ZFEC_HIP_GENERIC=0 / 1 starts in mode 0 /
- * 1).  Returns the previous mode; any other value only queries.  Results are
+ * kernels serve them; environment ZFEC_HIP_GENERIC=0 / 1 / 2 starts in that
+ * mode).  Returns the previous mode; any other value only queries.  Results are
  * bit-identical in every mode. */
 int fec_generic_mode(int mode);
 

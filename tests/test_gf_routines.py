@@ -20,6 +20,8 @@ from oracle import oracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INC = os.path.join(ROOT, "zfec_amd", "csrc", "gf_routines.inc")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from gen_gf_routines import ACC, PL  # noqa: E402  (the register contract)
 
 
 def test_generated_file_is_current():
@@ -59,17 +61,17 @@ def test_every_routine_multiplies():
             acc0 = rng.integers(0, 256, size=32, dtype=np.uint8)
             v = {}
             for b, pl in enumerate(_planes(x)):
-                v[104 + b] = pl
+                v[PL + b] = pl
             for d, a, b in xors:
                 v[d] = v[a] ^ v[b]
             for b, pl in enumerate(_planes(acc0)):
-                v[24 + b] = pl
+                v[ACC + b] = pl
             for ln in body:
                 m = op.fullmatch(ln)
                 assert m, (c, ln)
                 d, s0, s1, s2 = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)
-                assert d == s0 and 24 <= d < 32, (c, ln)
+                assert d == s0 and ACC <= d < ACC + 8, (c, ln)
                 val = lambda s: 0 if s == "0" else v[int(s[1:])]
                 v[d] = v[s0] ^ val(s1) ^ val(s2)
             want = _planes(acc0 ^ mul[c][x])
-            assert [v[24 + b] for b in range(8)] == want, (c, trial)
+            assert [v[ACC + b] for b in range(8)] == want, (c, trial)

@@ -24,6 +24,9 @@
 //                       caller): each workgroup expands its coefficients into
 //                       LDS tables from a compile-time bank of all 256 values;
 //                       rows in register tiles, inputs in prefetched groups.
+//   matapply_bsr<RT>    bit-sliced, coefficients as run-time data, k <= 32,
+//                       r <= 40: one call per coefficient into precompiled
+//                       multiply-by-constant routines (gf_routines.inc).
 //   matapply_bsg        bit-sliced, coefficients as run-time data, k <= 256
 //                       (past 32 inputs its pointers and coefficients come
 //                       from a device-side table).
@@ -1111,20 +1114,28 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 // instructions for every c as a routine (zfec_gf_routines + 72 c) working on
 // fixed registers: the input's combinations of planes (built once per input
 // per wave) and accumulator row 0, offset to row rr by VGPR index mode.  A
-// coefficient costs a call (five scalar instructions and two jumps, no LDS
+// coefficient costs a call (a few scalar instructions and two jumps, no LDS
 // read) instead of matapply_bsg's sixteen LDS reads or a compile per matrix.
 //
-// Workgroup = one unit (2 KiB of every block of a stripe, 32 bytes per lane,
-// like the JIT kernels) and nw waves, one per row tile of <= RT rows: the waves
-// first load, transpose and park the unit's k inputs as bit-planes in LDS
-// (k * 2 KiB, each wave a k / nw share), then each walks all k inputs for its
-// tile.  Coefficients: MatJob::coef as [wave][input][RTP] bytes (RTP = RT
-// rounded up to 4, rows past the tile 0: routine 0 only returns).
+// Unit = 2 KiB of every block of a stripe (32 bytes per lane, like the JIT
+// kernels); rows in tiles of <= RT <= 10 (the accumulators of a tile live in
+// v54..v53+8RT).  Two forms:
+//   matapply_bsr_solo<RT> (one tile, r <= 10): one wave per unit, no LDS; the
+//       wave loads and transposes its inputs two ahead;
+//   matapply_bsr<RT> ("lds", r > 10): one workgroup per unit, a wave per
+//       tile; phases of kBsrPhase inputs: the waves load and transpose a
+//       phase's inputs into LDS planes (16 KiB), then each walks them for its
+//       tile.  All k inputs in LDS at once (k * 2 KiB) capped the workgroups
+//       per CU and measured 0.51 ms against 0.37-0.38 with phases of 8 on
+//       cfg4's first-seen decodes (profiles/r04_bsr_ab.json).
+// Coefficients: MatJob::coef as [tile][input][RTP] bytes (RTP = RT rounded up
+// to 4, rows past the tile 0: routine 0 only returns).
 // ---------------------------------------------------------------------------
 #include "gf_routines.inc"
 
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
-constexpr int kBsrBatch = 8;          // inputs a wave loads at once
+constexpr int kBsrBatch = 4;          // inputs a wave loads at once
+constexpr uint32_t kBsrPhase = 8;     // inputs whose planes share LDS at a time (multi-wave form)
 
 template <int RT>
 __host__ __device__ constexpr uint32_t bsr_rtp() {
@@ -1132,14 +1143,14 @@ __host__ __device__ constexpr uint32_t bsr_rtp() {
 }
 
 template <int RT>
-__global__ __launch_bounds__(256) void matapply_bsr(const MatJob job) {
+__global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
     constexpr uint32_t RTP = bsr_rtp<RT>();
     extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
-    const uint32_t kp = job.pad_ ? job.pad_ : k;  // inputs per LDS phase
+    constexpr uint32_t kp = kBsrPhase;
     const uint32_t r0 = wave * r / nw, rows = (wave + 1) * r / nw - r0;
     const KPtr<MatJob> kj = kernarg_job<MatJob>();
     const KWords cw = (KWords)kj->coef + wave * k * (RTP / 4);
@@ -1865,12 +1876,14 @@ std::once_flag g_bsr_once;
 template <int RT>
 void fill_bsr() {
     g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT>);
-    snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d>", RT);
+    snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d,lds>", RT);
     g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
-    snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d,solo>", RT);
+    snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d>", RT);
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
 }
 
+// Row tiles of at most 10 rows (8 and 7 measured the same on cfg4's first-seen
+// decodes, profiles/r04_bsr_ab.json).
 void bsr_tiles(uint32_t r, uint32_t* nw, uint32_t* rt) {
     *nw = (r + kBsrMaxRows - 1) / kBsrMaxRows;
     *rt = (r + *nw - 1) / *nw;
@@ -1882,7 +1895,7 @@ bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
         return false;
     uint32_t nw, rt;
     bsr_tiles(r, &nw, &rt);
-    return nw * k * ((rt + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
+    return nw <= 8 && nw * k * ((rt + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
 }
 
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
@@ -1908,23 +1921,14 @@ hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
-    static const uint32_t kp_env = [] {
-        const char* e = getenv("ZFEC_HIP_BSR_KP");
-        return e ? static_cast<uint32_t>(atoi(e)) : 0u;
-    }();
-    static const bool solo = [] {
-        const char* e = getenv("ZFEC_HIP_BSR_SOLO");
-        return e && e[0] == '1';
-    }();
-    if (solo) {
-        job.pad_ = nw;
-        const uint64_t vu = units * nw;
+    if (nw == 1) {  // one row tile: one wave per unit, no LDS
+        job.pad_ = 1;
         const uint64_t capw = uint64_t(g_num_cu) * 64;
         t_last_kernel = g_bsr_var[rt].name_solo;
-        return launch_job(g_bsr_var[rt].fn_solo, static_cast<uint32_t>(vu < capw ? vu : capw), 64, 0, stream, job);
+        return launch_job(g_bsr_var[rt].fn_solo, static_cast<uint32_t>(units < capw ? units : capw), 64, 0, stream,
+                          job);
     }
-    const uint32_t kp = kp_env && kp_env < k ? kp_env : k;
-    job.pad_ = kp;
+    const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
     t_last_kernel = g_bsr_var[rt].name;
     return launch_job(g_bsr_var[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job);
 }
@@ -1935,7 +1939,7 @@ int generic_mode() {
     int g = g_generic.load();
     if (g < 0) {
         const char* e = getenv("ZFEC_HIP_GENERIC");
-        g = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 1;
+        g = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 2;
         int expect = -1;
         if (!g_generic.compare_exchange_strong(expect, g)) g = expect;  // set_generic_mode won the race
     }

@@ -109,8 +109,8 @@ const char* matapply_last_kernel();
 // The bit-sliced kernels with the coefficients as run-time data, for wide-code
 // launches that no specialised JIT kernel serves: 2 = matapply_bsr where its
 // shape fits (k <= 32, r <= 40), else matapply_bsg (default); 1 = matapply_bsg
-// only; 0 = off (the table kernels serve).  Env ZFEC_HIP_GENERIC=0/1 starts
-// in mode 0/1.
+// only; 0 = off (the table kernels serve).  Env ZFEC_HIP_GENERIC=0/1/2 starts
+// in that mode.
 int generic_mode();
 void set_generic_mode(int mode);
 
