@@ -301,7 +301,7 @@ VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4.25
 # Device code the committed counter summaries describe: a summary is used only
 # when it was collected on these exact sources (tools/pmc_sq_summary.py).
 DEVICE_SOURCES = ("zfec_amd/csrc/kernels.hip", "zfec_amd/csrc/kernels.hpp", "zfec_amd/csrc/bitslice.cpp",
-                  "zfec_amd/csrc/bitslice.hpp")
+                  "zfec_amd/csrc/bitslice.hpp", "zfec_amd/csrc/gf_routines.inc")
 
 
 def device_tree_hash():
