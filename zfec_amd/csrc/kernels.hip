@@ -1195,18 +1195,16 @@ __global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
             __syncthreads();
             // input j's planes and coefficient words are read during input j - 1
             // (one wait drains LDS and scalar loads alike)
-            u32x4 pa = bsr_planes[lane], pb = bsr_planes[64u + lane];
             uint32_t cwd[RTP / 4];
 #pragma unroll
             for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[ph * (RTP / 4) + d];
             for (uint32_t j = 0; j < kn; ++j) {
+                const u32x4 pa = bsr_planes[j * 128u + lane], pb = bsr_planes[j * 128u + 64u + lane];
                 const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
                 uint32_t offs[RT];
 #pragma unroll
                 for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
                 if (j + 1 < kn) {
-                    pa = bsr_planes[(j + 1) * 128u + lane];
-                    pb = bsr_planes[(j + 1) * 128u + 64u + lane];
 #pragma unroll
                     for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(ph + j + 1) * (RTP / 4) + d];
                 }
@@ -1916,14 +1914,14 @@ hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
             for (uint32_t rr = 0; rr < rows; ++rr)
                 job.coef[(w * k + j) * rtp + rr] = a.coef[size_t(r0 + rr) * a.coef_stride + j];
     }
-    const uint64_t cap = uint64_t(g_num_cu) * 32;
+    const uint64_t cap = uint64_t(g_num_cu) * 1024;
     const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
     if (nw == 1) {  // one row tile: one wave per unit, no LDS
         job.pad_ = 1;
-        const uint64_t capw = uint64_t(g_num_cu) * 64;
+        const uint64_t capw = uint64_t(g_num_cu) * 1024;
         t_last_kernel = g_bsr_var[rt].name_solo;
         return launch_job(g_bsr_var[rt].fn_solo, static_cast<uint32_t>(units < capw ? units : capw), 64, 0, stream,
                           job);
