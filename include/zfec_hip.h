@@ -244,9 +244,9 @@ int fec_jit_mode(int mode);
 /* Wide-code launches that no compiled specialised kernel serves (a decode of
  * an erasure pattern seen for the first time, small launches, JIT off) run on
  * the bit-sliced kernels that take the coefficient matrix as run-time data (no
- * compile step): mode 2 = matapply_bsr where it fits (k <= 32, r <= 40; the
- * specialised kernels' instruction stream, one call per coefficient), else
- * matapply_bsg (default); 1 = matapply_bsg only; 0 = off (the table-lookup
+ * compile step): mode 2 = matapply_bsr (default; the specialised kernels'
+ * instruction stream, one call per coefficient, any k, r up to 256/256);
+ * 1 = matapply_bsg only; 0 = off (the table-lookup
  * kernels serve them; environment ZFEC_HIP_GENERIC=0 / 1 / 2 starts in that
  * mode).  Returns the previous mode; any other value only queries.  Results are
  * bit-identical in every mode. */

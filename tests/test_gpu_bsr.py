@@ -200,3 +200,165 @@ def test_bsr_equals_bsg(k, m):
         capi.jit_mode(prev_j)
     assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
     assert (res[2][1].numpy() == data).all()
+
+
+# k > 32 with one row tile: matapply_bsr_ks (inputs split over the waves of a
+# workgroup, partial planes XOR-reduced in LDS, pointers and coefficients from
+# a device-side table); the reference benchmark's own shape is 94/100
+# (benchmark-zfec/Main.hs:17)
+WIDE_SHAPES = [(33, 34), (40, 48), (47, 57), (94, 100), (128, 131), (200, 206), (255, 256)]
+
+
+@pytest.mark.parametrize("k,m", WIDE_SHAPES)
+def test_bsr_wide_vs_oracle(bsr_only, k, m):
+    rng = np.random.default_rng(k * 7 + m)
+    for sz in (4096, 6001, 70000):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name() == "matapply_bsr<%d,ks,tbl>" % (m - k), capi.last_kernel_name()
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz, nums)
+
+
+def test_bsr_wide_batched_guards(bsr_only):
+    """94/100 over strided stripes at misaligned bases: every stripe against the
+    oracle, bytes between rows and around the buffer untouched."""
+    k, m, sz, ns = 94, 100, 5000, 5
+    r = m - k
+    rng = np.random.default_rng(9400)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    ld = sz + 40
+    src = torch.zeros(7 + ns * k * ld, dtype=torch.uint8, device="cuda")
+    src[7:].view(ns, k, ld)[:, :, :sz] = torch.from_numpy(data).cuda()
+    dst = torch.full((9 + ns * r * ld + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    code.encode_batch(src.data_ptr() + 7, ld, k * ld, dst.data_ptr() + 9, ld, r * ld, list(range(k, m)), sz, ns,
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name() == "matapply_bsr<6,ks,tbl>", capi.last_kernel_name()
+    d = dst.cpu().numpy()
+    assert (d[:9] == 0xA5).all() and (d[9 + ns * r * ld:] == 0xA5).all()
+    o = d[9:9 + ns * r * ld].reshape(ns, r, ld)
+    assert (o[:, :, sz:] == 0xA5).all(), "write past a row"
+    for s_ in range(ns):
+        assert (o[s_, :, :sz] == oracle.encode(k, m, data[s_])).all(), s_
+
+
+def test_bsr_wide_table_ring_reuse(bsr_only):
+    """More wide launches than the table ring has slots, queued back to back on
+    one stream with different matrices: each launch must read its own table."""
+    k, m, sz = 94, 100, 8192
+    rng = np.random.default_rng(941)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    allb = zfec_amd.Encoder(k, m).encode(ins)
+    dec = zfec_amd.Decoder(k, m)
+    results = []
+    for _ in range(20):  # 20 > 8 ring slots
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        results.append((nums, dec.decode([allb[n] for n in nums], nums)))
+    torch.cuda.synchronize()
+    for nums, got in results:
+        assert (torch.stack(got).cpu().numpy() == data).all(), nums
+
+
+@pytest.mark.parametrize("k,m", [(94, 100), (255, 256)])
+def test_bsr_wide_equals_bsg(k, m):
+    """Generic mode 2 (matapply_bsr_ks) and 1 (matapply_bsg's table form) on the
+    same encode: identical bytes."""
+    rng = np.random.default_rng(k)
+    sz = 70000
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    prev_j = capi.jit_mode(capi.JIT_OFF)
+    res = {}
+    try:
+        for gen in (2, 1):
+            prev = capi.generic_mode(gen)
+            try:
+                res[gen] = torch.stack(zfec_amd.Encoder(k, m).encode(ins)[k:]).cpu()
+                torch.cuda.synchronize()
+                assert capi.last_kernel_name().startswith("matapply_bsr" if gen == 2 else "matapply_bsg")
+            finally:
+                capi.generic_mode(prev)
+    finally:
+        capi.jit_mode(prev_j)
+    assert torch.equal(res[1], res[2])
+
+
+def tbl_name(r, units, k):
+    """matapply_bsr's table form: tiles of <= 8 rows (<= 4 for k > 64 when
+    units x tiles gives fewer than 16 waves per CU), row groups of <= 8 tiles."""
+    tile = 4 if k > 64 and units * -(-r // 8) < 256 * 16 else 8
+    ng = -(-r // (8 * tile))
+    rpg = -(-r // ng)
+    nw = -(-rpg // tile)
+    return "matapply_bsr<%d,lds,tbl>" % (-(-rpg // nw))
+
+
+# table form of the LDS-phase kernel: k > 32 with more than one row tile (row
+# groups of <= 64 rows past 64), and k <= 32 with 41..48 rows
+TBL_SHAPES = [(33, 50), (40, 60), (47, 60), (64, 112), (128, 150), (128, 256), (200, 256), (32, 74), (20, 68)]
+
+
+@pytest.mark.parametrize("k,m", [(40, 60), (128, 256)])
+def test_bsr_table_form_large_launch(bsr_only, k, m):
+    """Enough units for tiles of 8 rows (128 / 64 MiB stripes): against the
+    oracle on sampled columns."""
+    rng = np.random.default_rng(k + 3 * m)
+    sz = ((128 if k < 64 else 64) << 20) // k
+    data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda")
+    out = zfec_amd.Encoder(k, m).encode([data[i] for i in range(k)])
+    torch.cuda.synchronize()
+    units = -(-sz // 2048)
+    assert capi.last_kernel_name() == tbl_name(m - k, units, k), capi.last_kernel_name()
+    cols = np.sort(rng.choice(sz, size=4096, replace=False))
+    got = torch.stack(out[k:])[:, torch.from_numpy(cols).cuda()].cpu().numpy()
+    want = oracle.encode(k, m, data[:, torch.from_numpy(cols).cuda()].cpu().numpy())
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("k,m", TBL_SHAPES)
+def test_bsr_table_form_vs_oracle(bsr_only, k, m):
+    rng = np.random.default_rng(k * 13 + m)
+    for sz in (4096, 6001):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name() == tbl_name(m - k, -(-sz // 2048), k), (capi.last_kernel_name(), k, m)
+        par = torch.stack(out[k:]).cpu().numpy()
+        assert (par == oracle.encode(k, m, data)).all(), (k, m, sz)
+        nums = sorted(int(x) for x in rng.choice(m, size=k, replace=False))
+        dec = zfec_amd.Decoder(k, m).decode([out[n] for n in nums], nums)
+        assert (torch.stack(dec).cpu().numpy() == data).all(), (k, m, sz, nums)
+
+
+def test_bsr_table_form_batched_guards(bsr_only):
+    """128/256 (two row groups) over strided stripes at misaligned bases: every
+    stripe against the oracle, bytes between rows and around the buffer
+    untouched."""
+    k, m, sz, ns = 128, 256, 4500, 3
+    r = m - k
+    rng = np.random.default_rng(128256)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    ld = sz + 40
+    src = torch.zeros(7 + ns * k * ld, dtype=torch.uint8, device="cuda")
+    src[7:].view(ns, k, ld)[:, :, :sz] = torch.from_numpy(data).cuda()
+    dst = torch.full((9 + ns * r * ld + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    code.encode_batch(src.data_ptr() + 7, ld, k * ld, dst.data_ptr() + 9, ld, r * ld, list(range(k, m)), sz, ns,
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name() == tbl_name(r, ns * -(-sz // 2048), k), capi.last_kernel_name()
+    d = dst.cpu().numpy()
+    assert (d[:9] == 0xA5).all() and (d[9 + ns * r * ld:] == 0xA5).all()
+    o = d[9:9 + ns * r * ld].reshape(ns, r, ld)
+    assert (o[:, :, sz:] == 0xA5).all(), "write past a row"
+    for s_ in range(ns):
+        assert (o[s_, :, :sz] == oracle.encode(k, m, data[s_])).all(), s_

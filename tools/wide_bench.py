@@ -9,7 +9,9 @@ over a rotation of disjoint buffer sets spanning >= 768 MiB.
 Variants: "shipped" -- the library as shipped in auto mode, after its
 background compiles (jit_wait): one pass over all k inputs per row group of
 <= 48 (matapply_bsg's device-side table, or a specialised JIT kernel up to
-1600 coefficients); "passes" -- round 2's path, the table kernels in
+1600 coefficients); "generic" -- JIT off, what serves a first-seen matrix
+(generic mode 2: matapply_bsr where it fits, else matapply_bsg); "bsg" -- JIT
+off, matapply_bsg only; "passes" -- round 2's path, the table kernels in
 XOR-accumulating passes of 32 inputs (generic kernel and JIT off).  The
 decodes are checked against the stripe every time.
 
@@ -29,6 +31,11 @@ import bench  # noqa: E402  (back_to_back, COLD_SPAN, HBM peak)
 from zfec_amd import capi  # noqa: E402
 
 
+# variant -> (JIT mode, generic mode)
+VARIANTS = {"shipped": (capi.JIT_AUTO, 2), "generic": (capi.JIT_OFF, 2), "bsg": (capi.JIT_OFF, 1),
+            "passes": (capi.JIT_OFF, 0)}
+
+
 def run_shape(k, m, launches, variant):
     r = m - k
     sz = -(-(64 << 20) // k)
@@ -45,10 +52,8 @@ def run_shape(k, m, launches, variant):
     code = capi.Code(k, m)
     nums = list(range(k, m))
     st = torch.cuda.current_stream()
-    if variant == "passes":
-        pj, pg = capi.jit_mode(capi.JIT_OFF), capi.generic_mode(0)
-    else:
-        pj, pg = capi.jit_mode(capi.JIT_AUTO), capi.generic_mode(1)
+    jit, gen = VARIANTS[variant]
+    pj, pg = capi.jit_mode(jit), capi.generic_mode(gen)
 
     def enc_i(i):
         def f(sh):

@@ -24,9 +24,11 @@
 //                       caller): each workgroup expands its coefficients into
 //                       LDS tables from a compile-time bank of all 256 values;
 //                       rows in register tiles, inputs in prefetched groups.
-//   matapply_bsr<RT>    bit-sliced, coefficients as run-time data, k <= 32,
-//                       r <= 40: one call per coefficient into precompiled
-//                       multiply-by-constant routines (gf_routines.inc).
+//   matapply_bsr<RT>    bit-sliced, coefficients as run-time data, any
+//                       k <= 256, r <= 256: one call per coefficient into
+//                       precompiled multiply-by-constant routines
+//                       (gf_routines.inc); past 32 inputs or 40 rows its
+//                       pointers and coefficients come from a device-side table.
 //   matapply_bsg        bit-sliced, coefficients as run-time data, k <= 256
 //                       (past 32 inputs its pointers and coefficients come
 //                       from a device-side table).
@@ -1142,8 +1144,19 @@ __host__ __device__ constexpr uint32_t bsr_rtp() {
     return (RT + 3) / 4 * 4;
 }
 
-template <int RT>
-__global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
+// Block pointers and coefficients of a table-form matapply_bsr launch
+// (k > 32 or more rows than one workgroup's tiles hold): a device-side table
+// the host fills per launch (TableRing), read with scalar loads.
+struct alignas(16) BsrTblJob {
+    uint64_t sz, in_sstride, out_sstride;
+    uint32_t nstripes, k, r, cps, gs_c, gs_s;
+    uint32_t ngroups;  // row groups (LDS form): workgroup units are (group, stripe, unit) triples
+    uint32_t pad_;
+    const uint8_t* table;
+};
+
+template <int RT, bool TBL, class J>
+__global__ __launch_bounds__(512) void matapply_bsr(const J job) {
     constexpr uint32_t RTP = bsr_rtp<RT>();
     extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
     const uint32_t lane = threadIdx.x & 63u;
@@ -1151,16 +1164,47 @@ __global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
     constexpr uint32_t kp = kBsrPhase;
-    const uint32_t r0 = wave * r / nw, rows = (wave + 1) * r / nw - r0;
-    const KPtr<MatJob> kj = kernarg_job<MatJob>();
-    const KWords cw = (KWords)kj->coef + wave * k * (RTP / 4);
+    // block pointers and coefficients: kernel arguments (MatJob) or the
+    // device-side table (BsrTblJob: k input and r output pointers, then per
+    // row group and wave [input][RTP] coefficient bytes); the walk's "stripes"
+    // are (row group, stripe) pairs, group-major
+    const uint32_t ns = job.nstripes;
+    uint32_t ng = 1;
+    CU64 tp = nullptr;
+    KPtr<MatJob> kj = nullptr;
+    if constexpr (TBL) {
+        ng = job.ngroups;
+        tp = (CU64)job.table;
+    } else {
+        kj = kernarg_job<MatJob>();
+    }
+    auto in_ptr = [&](uint32_t j) -> const uint8_t* {
+        if constexpr (TBL)
+            return reinterpret_cast<const uint8_t*>(tp[j]);
+        else
+            return kj->in[j];
+    };
+    auto out_ptr = [&](uint32_t i) -> uint8_t* {
+        if constexpr (TBL)
+            return reinterpret_cast<uint8_t*>(tp[k + i]);
+        else
+            return kj->out[i];
+    };
     const uint64_t sz = job.sz;
     uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
-    while (s < job.nstripes) {
+    while (s < ns * ng) {
+        const uint32_t g = TBL ? s / ns : 0u, stripe = TBL ? s - g * ns : s;
+        const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
+        const uint32_t r0 = gr0 + wave * grn / nw, rows = gr0 + (wave + 1) * grn / nw - r0;
+        KWords cw;
+        if constexpr (TBL)
+            cw = (KWords)(tp + k + r) + (g * nw + wave) * k * (RTP / 4);
+        else
+            cw = (KWords)kj->coef + wave * k * (RTP / 4);
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;  // the last unit ends at sz (overlapping its neighbour)
-        const uint64_t ib = s * job.in_sstride + off + lane * 16u;
-        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
+        const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
         uint32_t acc[RT][8];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr)
@@ -1175,7 +1219,7 @@ __global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
                 for (int q = 0; q < kBsrBatch; ++q) {
                     const uint32_t j = j0 + q * nw;
                     if (j < kn) {  // wave-uniform
-                        const uint8_t* ip = kj->in[ph + j] + ib;
+                        const uint8_t* ip = in_ptr(ph + j) + ib;
                         x[q][0] = load16(ip);
                         x[q][1] = load16(ip + 1024);
                     }
@@ -1216,7 +1260,7 @@ __global__ __launch_bounds__(512) void matapply_bsr(const MatJob job) {
         for (int rr = 0; rr < RT; ++rr) {
             if (static_cast<uint32_t>(rr) < rows) {  // wave-uniform
                 transpose8(acc[rr]);
-                uint8_t* op = kj->out[r0 + rr] + ob;
+                uint8_t* op = out_ptr(r0 + rr) + ob;
                 store16_out<true>(op, u32x4{acc[rr][0], acc[rr][1], acc[rr][2], acc[rr][3]});
                 store16_out<true>(op + 1024, u32x4{acc[rr][4], acc[rr][5], acc[rr][6], acc[rr][7]});
             }
@@ -1291,6 +1335,102 @@ __global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
                 store16_out<true>(op, u32x4{acc[rr][0], acc[rr][1], acc[rr][2], acc[rr][3]});
                 store16_out<true>(op + 1024, u32x4{acc[rr][4], acc[rr][5], acc[rr][6], acc[rr][7]});
             }
+        }
+    }
+}
+
+// Wide codes (k > 32) with one row tile (r <= 10), e.g. the reference
+// benchmark's 94/100: a 64 MiB stripe is only a few hundred 2 KiB units, so
+// the W waves of a workgroup split a unit's inputs (wave w: inputs
+// [w k / W, (w + 1) k / W), loaded two ahead and transposed by the wave), XOR
+// their partial accumulator planes into one LDS copy of the unit's rows
+// (ds_xor_b32, [row][plane][lane]), and after a barrier wave w transposes and
+// stores rows w, w + W, ...  Block pointers and coefficients come from a
+// device-side table (BsrTblJob::table: k input pointers, r output pointers,
+// then [input][RTP] coefficient bytes).
+template <int RT>
+__global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
+    constexpr uint32_t RTP = bsr_rtp<RT>();
+    __shared__ uint32_t red[RT * 8 * 64];  // [row][plane][lane]
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = blockDim.x >> 6;
+    const uint32_t k = job.k, r = job.r;
+    const CU64 tp = (CU64)job.table;
+    const KWords cw = (KWords)(tp + k + r);
+    const uint32_t j0 = wave * k / nw, j1 = (wave + 1) * k / nw;
+    const uint64_t sz = job.sz;
+    for (uint32_t i = threadIdx.x; i < RT * 8 * 64; i += blockDim.x) red[i] = 0u;
+    __syncthreads();
+    uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
+    while (s < job.nstripes) {
+        uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
+        if (off > sz - kBsrChunk) off = sz - kBsrChunk;
+        const uint64_t ib = s * job.in_sstride + off + lane * 16u;
+        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        if (j0 < j1) {  // wave-uniform
+            uint32_t acc[RT][8];
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr)
+#pragma unroll
+                for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
+            const uint8_t* ip0 = reinterpret_cast<const uint8_t*>(tp[j0]) + ib;
+            u32x4 a0 = load16(ip0), a1 = load16(ip0 + 1024);
+            u32x4 b0 = a0, b1 = a1;
+            if (j0 + 1 < j1) {
+                const uint8_t* ip1 = reinterpret_cast<const uint8_t*>(tp[j0 + 1]) + ib;
+                b0 = load16(ip1);
+                b1 = load16(ip1 + 1024);
+            }
+            uint32_t cwd[RTP / 4];
+#pragma unroll
+            for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[j0 * (RTP / 4) + d];
+            for (uint32_t j = j0; j < j1; ++j) {
+                uint32_t p[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                a0 = b0;
+                a1 = b1;
+                if (j + 2 < j1) {
+                    const uint8_t* ip = reinterpret_cast<const uint8_t*>(tp[j + 2]) + ib;
+                    b0 = load16(ip);
+                    b1 = load16(ip + 1024);
+                }
+                transpose8(p);
+                uint32_t offs[RT];
+#pragma unroll
+                for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
+                if (j + 1 < j1) {
+#pragma unroll
+                    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(j + 1) * (RTP / 4) + d];
+                }
+                bsr_input<RT>(acc, p, offs);
+            }
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr)
+                if (static_cast<uint32_t>(rr) < r)
+#pragma unroll
+                    for (int b = 0; b < 8; ++b)
+                        __hip_atomic_fetch_xor(&red[(rr * 8 + b) * 64 + lane], acc[rr][b], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+        for (uint32_t i = wave; i < r; i += nw) {  // wave-uniform
+            uint32_t v[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                v[b] = red[(i * 8 + b) * 64 + lane];
+                red[(i * 8 + b) * 64 + lane] = 0u;  // ready for the next unit
+            }
+            transpose8(v);
+            uint8_t* op = reinterpret_cast<uint8_t*>(tp[k + i]) + ob;
+            store16_out<true>(op, u32x4{v[0], v[1], v[2], v[3]});
+            store16_out<true>(op + 1024, u32x4{v[4], v[5], v[6], v[7]});
+        }
+        __syncthreads();  // rows read and cleared before the next unit's partials
+        c += job.gs_c;
+        s += job.gs_s;
+        if (c >= job.cps) {
+            c -= job.cps;
+            ++s;
         }
     }
 }
@@ -1873,7 +2013,7 @@ std::once_flag g_bsr_once;
 
 template <int RT>
 void fill_bsr() {
-    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT>);
+    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, false, MatJob>);
     snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d,lds>", RT);
     g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
     snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d>", RT);
@@ -1894,6 +2034,162 @@ bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
     uint32_t nw, rt;
     bsr_tiles(r, &nw, &rt);
     return nw <= 8 && nw * k * ((rt + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
+}
+
+// Wide codes, one row tile: matapply_bsr_ks (table form).  Waves per unit:
+// enough for ~8 waves per CU over the launch, 4-8, at least 4 inputs each.
+bool bsr_wide_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    return generic_mode() == 2 && k > static_cast<uint32_t>(kMaxIn) && k <= static_cast<uint32_t>(kMaxWideIn) &&
+           r >= 1 && r <= static_cast<uint32_t>(kBsrMaxRows) && sz >= kBsgChunk && k * r >= 24;
+}
+
+struct BsrKsVariant {
+    const void* fn = nullptr;
+    char name[28] = "";
+};
+BsrKsVariant g_bsr_ks[kBsrMaxRows + 1];
+std::once_flag g_bsr_ks_once;
+
+template <int RT>
+void fill_bsr_ks() {
+    g_bsr_ks[RT].fn = reinterpret_cast<const void*>(matapply_bsr_ks<RT>);
+    snprintf(g_bsr_ks[RT].name, sizeof g_bsr_ks[RT].name, "matapply_bsr<%d,ks,tbl>", RT);
+    if constexpr (RT < kBsrMaxRows) fill_bsr_ks<RT + 1>();
+}
+
+hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
+    std::call_once(g_bsr_ks_once, [] { fill_bsr_ks<1>(); });
+    const uint32_t k = a.k, r = a.r, rt = r, rtp = (rt + 3) / 4 * 4;
+    const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
+    const uint64_t units = cps * a.nstripes;
+    if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
+    // waves per unit: 8 when the launch has fewer than 2 units per CU, else 4
+    // (>= 4 inputs per wave); 16 waves measured slower on 94/100 (0.027 ->
+    // 0.031 ms per 64 MiB stripe) and the same on 255/256
+    uint32_t nw = units * 2 < uint64_t(g_num_cu) * 4 ? 8u : 4u;
+    while (nw > 1 && k / nw < 4) nw /= 2;
+    const size_t bytes = 8 * size_t(k + r) + size_t(k) * rtp;
+    if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
+    TableRing* ring = nullptr;
+    unsigned slot = 0;
+    hipError_t e = ring_slot(&ring, &slot);
+    if (e != hipSuccess) return e;
+    uint8_t* h = ring->host + slot * TableRing::kSlotBytes;
+    uint8_t* d = ring->dev + slot * TableRing::kSlotBytes;
+    std::memcpy(h, a.in, 8 * size_t(k));
+    std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
+    uint8_t* cf = h + 8 * size_t(k + r);
+    std::memset(cf, 0, size_t(k) * rtp);
+    for (uint32_t j = 0; j < k; ++j)
+        for (uint32_t i = 0; i < r; ++i) cf[size_t(j) * rtp + i] = a.coef[size_t(i) * a.coef_stride + j];
+    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    BsrTblJob job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = k;
+    job.r = r;
+    const uint64_t cap = uint64_t(g_num_cu) * 1024;
+    const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_s = static_cast<uint32_t>(grid / cps);
+    job.gs_c = static_cast<uint32_t>(grid % cps);
+    job.table = d;
+    if ((e = launch_job(g_bsr_ks[rt].fn, grid, 64 * nw, 0, stream, job)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
+    ring->busy[slot] = true;
+    t_last_kernel = g_bsr_ks[rt].name;
+    return hipSuccess;
+}
+
+// Table form of the LDS-phase kernel: k > 32 with more than one row tile, or
+// more rows than 4 tiles of 10.  Tiles of <= 8 rows (<= 127 VGPRs: 4 waves per
+// SIMD), <= 8 waves per workgroup, so row groups of <= 64 rows; each group's
+// workgroups read the unit's inputs again (L2 when they run together).
+constexpr uint32_t kBsrTblTile = 8;
+
+bool bsr_tbl_ok(uint32_t k, uint32_t r, uint64_t sz) {
+    return generic_mode() == 2 && k >= 1 && k <= static_cast<uint32_t>(kMaxWideIn) && r >= 1 && r <= 256 &&
+           sz >= kBsgChunk && k * r >= 24 && !(k <= 4 && r <= 8) &&
+           (k > static_cast<uint32_t>(kMaxIn) ? r > static_cast<uint32_t>(kBsrMaxRows) : r > 4u * kBsrMaxRows);
+}
+
+struct BsrTblVariant {
+    const void* fn = nullptr;
+    char name[28] = "";
+};
+BsrTblVariant g_bsr_tbl[kBsrTblTile + 1];
+std::once_flag g_bsr_tbl_once;
+
+template <int RT>
+void fill_bsr_tbl() {
+    g_bsr_tbl[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, true, BsrTblJob>);
+    snprintf(g_bsr_tbl[RT].name, sizeof g_bsr_tbl[RT].name, "matapply_bsr<%d,lds,tbl>", RT);
+    if constexpr (RT < static_cast<int>(kBsrTblTile)) fill_bsr_tbl<RT + 1>();
+}
+
+hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
+    std::call_once(g_bsr_tbl_once, [] { fill_bsr_tbl<1>(); });
+    const uint32_t k = a.k, r = a.r;
+    const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
+    // tiles of <= 8 rows, or <= 4 for many inputs and too few units to give
+    // the CUs ~16 waves each (a wave per tile per unit): 200/256 0.176 -> 0.145
+    // ms per 64 MiB stripe; 40/60 0.051 -> 0.061, so not for few inputs
+    const uint64_t units1 = cps * a.nstripes;
+    const uint32_t tile =
+        k > 64 && units1 * ((r + kBsrTblTile - 1) / kBsrTblTile) < uint64_t(g_num_cu) * 16 ? 4u : kBsrTblTile;
+    const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
+    const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
+    const uint32_t nw = (rpg + tile - 1) / tile;
+    const uint32_t rt = (rpg + nw - 1) / nw, rtp = (rt + 3) / 4 * 4;
+    const uint64_t vunits = cps * a.nstripes * ng;
+    if (vunits >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
+    const size_t cbytes = size_t(ng) * nw * k * rtp;
+    const size_t bytes = 8 * size_t(k + r) + cbytes;
+    if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
+    TableRing* ring = nullptr;
+    unsigned slot = 0;
+    hipError_t e = ring_slot(&ring, &slot);
+    if (e != hipSuccess) return e;
+    uint8_t* h = ring->host + slot * TableRing::kSlotBytes;
+    uint8_t* d = ring->dev + slot * TableRing::kSlotBytes;
+    std::memcpy(h, a.in, 8 * size_t(k));
+    std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
+    uint8_t* cf = h + 8 * size_t(k + r);
+    std::memset(cf, 0, cbytes);
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t r0 = gr0 + w * grn / nw, rows = gr0 + (w + 1) * grn / nw - r0;
+            for (uint32_t j = 0; j < k; ++j)
+                for (uint32_t rr = 0; rr < rows; ++rr)
+                    cf[((size_t(g) * nw + w) * k + j) * rtp + rr] = a.coef[size_t(r0 + rr) * a.coef_stride + j];
+        }
+    }
+    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    BsrTblJob job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = k;
+    job.r = r;
+    job.ngroups = ng;
+    job.pad_ = 0;
+    const uint64_t cap = uint64_t(g_num_cu) * 1024;
+    const uint32_t grid = static_cast<uint32_t>(vunits < cap ? vunits : cap);
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_s = static_cast<uint32_t>(grid / cps);
+    job.gs_c = static_cast<uint32_t>(grid % cps);
+    job.table = d;
+    const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
+    if ((e = launch_job(g_bsr_tbl[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job)) != hipSuccess)
+        return e;
+    if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
+    ring->busy[slot] = true;
+    t_last_kernel = g_bsr_tbl[rt].name;
+    return hipSuccess;
 }
 
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
@@ -1994,6 +2290,8 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     const bool reg = k <= static_cast<uint32_t>(kRegK) && r <= static_cast<uint32_t>(kRegR);
     if (wide) {
         if (a.accumulate || !bsg_shape_ok(k, r, a.sz)) return hipErrorNotSupported;
+        if (bsr_wide_ok(k, r, a.sz)) return launch_bsr_wide(a, stream);
+        if (bsr_tbl_ok(k, r, a.sz)) return launch_bsr_tbl(a, stream);
         return launch_bsg(a, stream);
     }
     const Config& cfg = config();
@@ -2008,6 +2306,7 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
         }
     }
     if (!a.accumulate && bsr_shape_ok(k, r, a.sz)) return launch_bsr(a, stream);
+    if (!a.accumulate && bsr_tbl_ok(k, r, a.sz)) return launch_bsr_tbl(a, stream);
     if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);

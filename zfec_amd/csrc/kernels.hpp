@@ -107,9 +107,9 @@ const char* matapply_variant_name(uint32_t k, uint32_t r, bool accumulate);
 const char* matapply_last_kernel();
 
 // The bit-sliced kernels with the coefficients as run-time data, for wide-code
-// launches that no specialised JIT kernel serves: 2 = matapply_bsr where its
-// shape fits (k <= 32, r <= 40), else matapply_bsg (default); 1 = matapply_bsg
-// only; 0 = off (the table kernels serve).  Env ZFEC_HIP_GENERIC=0/1/2 starts
+// launches that no specialised JIT kernel serves: 2 = matapply_bsr (default;
+// matapply_bsg for the few shapes it does not take); 1 = matapply_bsg only;
+// 0 = off (the table kernels serve).  Env ZFEC_HIP_GENERIC=0/1/2 starts
 // in that mode.
 int generic_mode();
 void set_generic_mode(int mode);
