@@ -1357,17 +1357,20 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
     const CU64 tp = (CU64)job.table;
-    const KWords cw = (KWords)(tp + k + r);
     const uint32_t j0 = wave * k / nw, j1 = (wave + 1) * k / nw;
+    const uint32_t ns = job.nstripes, ng = job.ngroups;  // row groups of <= RT rows: (group, stripe) walk
     const uint64_t sz = job.sz;
     for (uint32_t i = threadIdx.x; i < RT * 8 * 64; i += blockDim.x) red[i] = 0u;
     __syncthreads();
     uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
-    while (s < job.nstripes) {
+    while (s < ns * ng) {
+        const uint32_t g = s / ns, stripe = s - g * ns;
+        const uint32_t gr0 = g * r / ng, rows = (g + 1) * r / ng - gr0;
+        const KWords cw = (KWords)(tp + k + r) + g * k * (RTP / 4);
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;
-        const uint64_t ib = s * job.in_sstride + off + lane * 16u;
-        const uint64_t ob = s * job.out_sstride + off + lane * 16u;
+        const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
+        const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
         if (j0 < j1) {  // wave-uniform
             uint32_t acc[RT][8];
 #pragma unroll
@@ -1406,14 +1409,14 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
             }
 #pragma unroll
             for (int rr = 0; rr < RT; ++rr)
-                if (static_cast<uint32_t>(rr) < r)
+                if (static_cast<uint32_t>(rr) < rows)
 #pragma unroll
                     for (int b = 0; b < 8; ++b)
                         __hip_atomic_fetch_xor(&red[(rr * 8 + b) * 64 + lane], acc[rr][b], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         __syncthreads();
-        for (uint32_t i = wave; i < r; i += nw) {  // wave-uniform
+        for (uint32_t i = wave; i < rows; i += nw) {  // wave-uniform
             uint32_t v[8];
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
@@ -1421,7 +1424,7 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
                 red[(i * 8 + b) * 64 + lane] = 0u;  // ready for the next unit
             }
             transpose8(v);
-            uint8_t* op = reinterpret_cast<uint8_t*>(tp[k + i]) + ob;
+            uint8_t* op = reinterpret_cast<uint8_t*>(tp[k + gr0 + i]) + ob;
             store16_out<true>(op, u32x4{v[0], v[1], v[2], v[3]});
             store16_out<true>(op + 1024, u32x4{v[4], v[5], v[6], v[7]});
         }
@@ -2038,9 +2041,30 @@ bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
 
 // Wide codes, one row tile: matapply_bsr_ks (table form).  Waves per unit:
 // enough for ~8 waves per CU over the launch, 4-8, at least 4 inputs each.
-bool bsr_wide_ok(uint32_t k, uint32_t r, uint64_t sz) {
-    return generic_mode() == 2 && k > static_cast<uint32_t>(kMaxIn) && k <= static_cast<uint32_t>(kMaxWideIn) &&
-           r >= 1 && r <= static_cast<uint32_t>(kBsrMaxRows) && sz >= kBsgChunk && k * r >= 24;
+constexpr uint32_t kBsrKsRows = 8;  // rows per group of the ks form past one tile
+constexpr uint32_t kBsrTblTile = 8;
+
+// Tile height of the table form of the LDS-phase kernel (below): 8 rows, or 4
+// for many inputs and too few units to give the CUs ~16 waves each (a wave per
+// tile per unit): 200/256 0.176 -> 0.145 ms per 64 MiB stripe; 40/60 0.051 ->
+// 0.061, so not for few inputs.
+uint32_t bsr_tbl_tile(uint32_t k, uint32_t r, uint64_t units) {
+    return k > 64 && units * ((r + kBsrTblTile - 1) / kBsrTblTile) < uint64_t(g_num_cu) * 16 ? 4u : kBsrTblTile;
+}
+
+// The ks form (inputs split over the waves of a workgroup) serves k > 32 with
+// one row tile, and -- in row groups of 8, each re-reading the inputs -- launches
+// of k >= 64 whose LDS-phase form would have fewer than 16 waves per CU:
+// 200/256 0.143 -> 0.095 ms, 64/112 0.086 -> 0.080; at 16 waves per CU the
+// re-reads cost more (128/256: 0.157 -> 0.195), and 40/60 is even (0.051 / 0.053).
+bool bsr_wide_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes) {
+    if (generic_mode() != 2 || k <= static_cast<uint32_t>(kMaxIn) || k > static_cast<uint32_t>(kMaxWideIn) || r < 1 ||
+        r > 256 || sz < kBsgChunk || k * r < 24)
+        return false;
+    if (r <= static_cast<uint32_t>(kBsrMaxRows)) return true;
+    const uint64_t units = (sz + kBsrChunk - 1) / kBsrChunk * nstripes;
+    const uint32_t tile = bsr_tbl_tile(k, r, units);
+    return k >= 64 && units * ((r + tile - 1) / tile) < uint64_t(g_num_cu) * 16;
 }
 
 struct BsrKsVariant {
@@ -2059,16 +2083,18 @@ void fill_bsr_ks() {
 
 hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_ks_once, [] { fill_bsr_ks<1>(); });
-    const uint32_t k = a.k, r = a.r, rt = r, rtp = (rt + 3) / 4 * 4;
+    const uint32_t k = a.k, r = a.r;
+    const uint32_t ng = r <= static_cast<uint32_t>(kBsrMaxRows) ? 1u : (r + kBsrKsRows - 1) / kBsrKsRows;
+    const uint32_t rt = (r + ng - 1) / ng, rtp = (rt + 3) / 4 * 4;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
-    const uint64_t units = cps * a.nstripes;
+    const uint64_t units = cps * a.nstripes * ng;
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
     // waves per unit: 8 when the launch has fewer than 2 units per CU, else 4
     // (>= 4 inputs per wave); 16 waves measured slower on 94/100 (0.027 ->
     // 0.031 ms per 64 MiB stripe) and the same on 255/256
     uint32_t nw = units * 2 < uint64_t(g_num_cu) * 4 ? 8u : 4u;
     while (nw > 1 && k / nw < 4) nw /= 2;
-    const size_t bytes = 8 * size_t(k + r) + size_t(k) * rtp;
+    const size_t bytes = 8 * size_t(k + r) + size_t(ng) * k * rtp;
     if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
     TableRing* ring = nullptr;
     unsigned slot = 0;
@@ -2079,9 +2105,13 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     std::memcpy(h, a.in, 8 * size_t(k));
     std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
     uint8_t* cf = h + 8 * size_t(k + r);
-    std::memset(cf, 0, size_t(k) * rtp);
-    for (uint32_t j = 0; j < k; ++j)
-        for (uint32_t i = 0; i < r; ++i) cf[size_t(j) * rtp + i] = a.coef[size_t(i) * a.coef_stride + j];
+    std::memset(cf, 0, size_t(ng) * k * rtp);
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t gr0 = g * r / ng, rows = (g + 1) * r / ng - gr0;
+        for (uint32_t j = 0; j < k; ++j)
+            for (uint32_t i = 0; i < rows; ++i)
+                cf[(size_t(g) * k + j) * rtp + i] = a.coef[size_t(gr0 + i) * a.coef_stride + j];
+    }
     if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
     BsrTblJob job;
     job.sz = a.sz;
@@ -2090,6 +2120,8 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     job.nstripes = static_cast<uint32_t>(a.nstripes);
     job.k = k;
     job.r = r;
+    job.ngroups = ng;
+    job.pad_ = 0;
     const uint64_t cap = uint64_t(g_num_cu) * 1024;
     const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
     job.cps = static_cast<uint32_t>(cps);
@@ -2107,8 +2139,6 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
 // more rows than 4 tiles of 10.  Tiles of <= 8 rows (<= 127 VGPRs: 4 waves per
 // SIMD), <= 8 waves per workgroup, so row groups of <= 64 rows; each group's
 // workgroups read the unit's inputs again (L2 when they run together).
-constexpr uint32_t kBsrTblTile = 8;
-
 bool bsr_tbl_ok(uint32_t k, uint32_t r, uint64_t sz) {
     return generic_mode() == 2 && k >= 1 && k <= static_cast<uint32_t>(kMaxWideIn) && r >= 1 && r <= 256 &&
            sz >= kBsgChunk && k * r >= 24 && !(k <= 4 && r <= 8) &&
@@ -2133,12 +2163,7 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_tbl_once, [] { fill_bsr_tbl<1>(); });
     const uint32_t k = a.k, r = a.r;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
-    // tiles of <= 8 rows, or <= 4 for many inputs and too few units to give
-    // the CUs ~16 waves each (a wave per tile per unit): 200/256 0.176 -> 0.145
-    // ms per 64 MiB stripe; 40/60 0.051 -> 0.061, so not for few inputs
-    const uint64_t units1 = cps * a.nstripes;
-    const uint32_t tile =
-        k > 64 && units1 * ((r + kBsrTblTile - 1) / kBsrTblTile) < uint64_t(g_num_cu) * 16 ? 4u : kBsrTblTile;
+    const uint32_t tile = bsr_tbl_tile(k, r, cps * a.nstripes);
     const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
     const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
     const uint32_t nw = (rpg + tile - 1) / tile;
@@ -2290,7 +2315,7 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     const bool reg = k <= static_cast<uint32_t>(kRegK) && r <= static_cast<uint32_t>(kRegR);
     if (wide) {
         if (a.accumulate || !bsg_shape_ok(k, r, a.sz)) return hipErrorNotSupported;
-        if (bsr_wide_ok(k, r, a.sz)) return launch_bsr_wide(a, stream);
+        if (bsr_wide_ok(k, r, a.sz, a.nstripes)) return launch_bsr_wide(a, stream);
         if (bsr_tbl_ok(k, r, a.sz)) return launch_bsr_tbl(a, stream);
         return launch_bsg(a, stream);
     }
