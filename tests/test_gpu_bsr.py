@@ -46,14 +46,16 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-def bsr_name(r):
-    nw = (r + 9) // 10
+def bsr_name(r, units=0):
+    """kernels.hip bsr_tiles: one wave for r <= 10; two for 11-16 rows, and
+    for 17-20 rows in launches of >= 2048 units; else four."""
+    nw = 1 if r <= 10 else 2 if r <= 16 or (r <= 20 and units * 2 >= 256 * 16) else 4
     return "matapply_bsr<%d>" % (-(-r // nw))
 
 
-def is_bsr(name, r):
+def is_bsr(name, r, units=0):
     """matapply_bsr<RT> for r rows (RT = rows per wave), any variant suffix."""
-    want = bsr_name(r)[:-1]
+    want = bsr_name(r, units)[:-1]
     return name.startswith(want) and name[len(want)] in ">,"
 
 

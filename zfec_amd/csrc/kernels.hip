@@ -2023,10 +2023,21 @@ void fill_bsr() {
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
 }
 
-// Row tiles of at most 10 rows (8 and 7 measured the same on cfg4's first-seen
-// decodes, profiles/r04_bsr_ab.json).
-void bsr_tiles(uint32_t r, uint32_t* nw, uint32_t* rt) {
-    *nw = (r + kBsrMaxRows - 1) / kBsrMaxRows;
+// Waves (row tiles) per workgroup: one for r <= 10 (the one-wave form); 4 for
+// r > 20 (tiles of <= 10 rows): 3 or 5 waves leave a SIMD of the CU with more
+// of them than the others (one 64 MiB stripe: 20/50 0.062 ms with 3 tiles of
+// 10 vs 0.056 with 4 of 8, 30/70 0.074 with 4 of 10 vs 0.091 with 5 of 8).
+// 11-16 rows: 2 tiles of <= 8 (20/33: 0.031 ms, 4 tiles 0.035); 17-20 rows: 2
+// tiles of 9-10 when the launch has units for >= 16 waves per CU (cfg4's
+// 1024-stripe r = 20 decode: 0.469 ms, 3 tiles 0.475-0.48), else 4 tiles of 5
+// (one 64 MiB 20/40 stripe: 0.044 ms, 2 tiles 0.053, 3 tiles 0.048).
+void bsr_tiles(uint32_t r, uint64_t units, uint32_t* nw, uint32_t* rt) {
+    if (r <= static_cast<uint32_t>(kBsrMaxRows))
+        *nw = 1;
+    else if (r <= 16 || (r <= 2u * kBsrMaxRows && units * 2 >= uint64_t(g_num_cu) * 16))
+        *nw = 2;
+    else
+        *nw = 4;
     *rt = (r + *nw - 1) / *nw;
 }
 
@@ -2034,9 +2045,10 @@ bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
     if (generic_mode() != 2 || k < 1 || k > static_cast<uint32_t>(kMaxIn) || r < 1 ||
         r > 4u * kBsrMaxRows || sz < kBsrChunk || k * r < 24 || (k <= 4 && r <= 8))
         return false;
-    uint32_t nw, rt;
-    bsr_tiles(r, &nw, &rt);
-    return nw <= 8 && nw * k * ((rt + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
+    // the largest coefficient block any launch of this shape lays out (4 tiles)
+    const uint32_t rt4 = (r + 3) / 4;
+    return r <= 4u * kBsrMaxRows && 4 * k * ((rt4 + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef) &&
+           2 * k * (((r + 1) / 2 + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
 }
 
 // Wide codes, one row tile: matapply_bsr_ks (table form).  Waves per unit:
@@ -2220,11 +2232,11 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_once, [] { fill_bsr<1>(); });
     const uint32_t k = a.k, r = a.r;
-    uint32_t nw, rt;
-    bsr_tiles(r, &nw, &rt);
-    const uint32_t rtp = (rt + 3) / 4 * 4;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
     const uint64_t units = cps * a.nstripes;
+    uint32_t nw, rt;
+    bsr_tiles(r, units, &nw, &rt);
+    const uint32_t rtp = (rt + 3) / 4 * 4;
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
     MatJob job;
     fill_matjob(a, job);
