@@ -305,7 +305,9 @@ def tbl_name(r, units, k):
         return "matapply_bsr<%d,ks,tbl>" % -(-r // ng)
     ng = -(-r // (8 * tile))
     rpg = -(-r // ng)
-    nw = -(-rpg // tile)
+    nw = 1
+    while nw * tile < rpg:
+        nw *= 2
     return "matapply_bsr<%d,lds,tbl>" % (-(-rpg // nw))
 
 

@@ -2178,7 +2178,8 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     const uint32_t tile = bsr_tbl_tile(k, r, cps * a.nstripes);
     const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
     const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
-    const uint32_t nw = (rpg + tile - 1) / tile;
+    uint32_t nw = 1;                                   // 1, 2, 4 or 8 waves: see bsr_tiles
+    while (nw * tile < rpg) nw *= 2;
     const uint32_t rt = (rpg + nw - 1) / nw, rtp = (rt + 3) / 4 * 4;
     const uint64_t vunits = cps * a.nstripes * ng;
     if (vunits >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
