@@ -1274,6 +1274,57 @@ __global__ __launch_bounds__(512) void matapply_bsr(const J job) {
     }
 }
 
+// One wave's walk over n inputs of a unit (the one-wave and ks forms): input
+// j's two 16-byte pieces at ptr(j) + ib, its coefficient words at cw[j * RTP/4].
+// Unrolled by two with fixed register roles (A: even inputs, B: odd), so a
+// load lands in the registers its input's transpose has just consumed (no
+// copies) and is waited for two inputs later; block pointers and coefficient
+// words are scalar-loaded one step ahead of their use (a scalar wait drains
+// every outstanding scalar load, so none is issued right before it is needed).
+template <int RT, class P>
+__device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uint64_t ib, KWords cw, P ptr) {
+    constexpr uint32_t RTP = bsr_rtp<RT>();
+    u32x4 a0, a1, b0, b1;
+    const uint8_t* pa = ptr(0);
+    const uint8_t* pb = ptr(n > 1 ? 1 : 0);
+    a0 = load16(pa + ib);
+    a1 = load16(pa + ib + 1024);
+    b0 = load16(pb + ib);
+    b1 = load16(pb + ib + 1024);
+    pa = ptr(n > 2 ? 2 : n - 1);
+    pb = ptr(n > 3 ? 3 : n - 1);
+    uint32_t cwd[RTP / 4];
+#pragma unroll
+    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[d];
+    // the loads and scalar loads are unconditional (past the last input they
+    // re-read input n - 1, from L2): a conditional load would make the compiler
+    // merge its registers with a copy that waits for every load in flight
+    auto step = [&](u32x4& x0, u32x4& x1, const uint8_t*& pn, uint32_t j) {
+        uint32_t p[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        transpose8(p);
+        uint32_t offs[RT];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
+        const uint32_t jn = j + 1 < n ? j + 1 : j;
+#pragma unroll
+        for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[jn * (RTP / 4) + d];
+        bsr_input<RT>(acc, p, offs);
+        // input j + 2 into x0 / x1, which the transpose has consumed (after the
+        // calls, so the compiler cannot keep the planes in them and copy)
+        x0 = load16(pn + ib);
+        x1 = load16(pn + ib + 1024);
+        pn = ptr(j + 4 < n ? j + 4 : n - 1);
+    };
+    // whole pairs, then an odd last input: with no conditional step inside the
+    // loop, input j's wait leaves input j + 1's loads in flight
+    uint32_t j = 0;
+    for (; j + 1 < n; j += 2) {
+        step(a0, a1, pa, j);
+        step(b0, b1, pb, j + 1);
+    }
+    if (j < n) step(a0, a1, pa, j);
+}
+
 // One wave per (unit, row tile), no LDS: the wave loads and transposes every
 // input of its unit itself (tiles of one unit are adjacent workgroups, so the
 // second tile's loads hit L2), two inputs in flight ahead.
@@ -1300,33 +1351,7 @@ __global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
         for (int rr = 0; rr < RT; ++rr)
 #pragma unroll
             for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
-        u32x4 a0 = load16(kj->in[0] + ib), a1 = load16(kj->in[0] + ib + 1024);
-        u32x4 b0 = a0, b1 = a1;
-        if (k > 1) {
-            b0 = load16(kj->in[1] + ib);
-            b1 = load16(kj->in[1] + ib + 1024);
-        }
-        uint32_t cwd[RTP / 4];
-#pragma unroll
-        for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[d];
-        for (uint32_t j = 0; j < k; ++j) {
-            uint32_t p[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            a0 = b0;
-            a1 = b1;
-            if (j + 2 < k) {
-                b0 = load16(kj->in[j + 2] + ib);
-                b1 = load16(kj->in[j + 2] + ib + 1024);
-            }
-            transpose8(p);
-            uint32_t offs[RT];
-#pragma unroll
-            for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
-            if (j + 1 < k) {
-#pragma unroll
-                for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(j + 1) * (RTP / 4) + d];
-            }
-            bsr_input<RT>(acc, p, offs);
-        }
+        bsr_walk<RT>(acc, k, ib, cw, [&](uint32_t j) { return kj->in[j]; });
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
             if (static_cast<uint32_t>(rr) < rows) {
@@ -1377,36 +1402,8 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
             for (int rr = 0; rr < RT; ++rr)
 #pragma unroll
                 for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
-            const uint8_t* ip0 = reinterpret_cast<const uint8_t*>(tp[j0]) + ib;
-            u32x4 a0 = load16(ip0), a1 = load16(ip0 + 1024);
-            u32x4 b0 = a0, b1 = a1;
-            if (j0 + 1 < j1) {
-                const uint8_t* ip1 = reinterpret_cast<const uint8_t*>(tp[j0 + 1]) + ib;
-                b0 = load16(ip1);
-                b1 = load16(ip1 + 1024);
-            }
-            uint32_t cwd[RTP / 4];
-#pragma unroll
-            for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[j0 * (RTP / 4) + d];
-            for (uint32_t j = j0; j < j1; ++j) {
-                uint32_t p[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                a0 = b0;
-                a1 = b1;
-                if (j + 2 < j1) {
-                    const uint8_t* ip = reinterpret_cast<const uint8_t*>(tp[j + 2]) + ib;
-                    b0 = load16(ip);
-                    b1 = load16(ip + 1024);
-                }
-                transpose8(p);
-                uint32_t offs[RT];
-#pragma unroll
-                for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
-                if (j + 1 < j1) {
-#pragma unroll
-                    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(j + 1) * (RTP / 4) + d];
-                }
-                bsr_input<RT>(acc, p, offs);
-            }
+            bsr_walk<RT>(acc, j1 - j0, ib, cw + j0 * (RTP / 4),
+                         [&](uint32_t j) { return reinterpret_cast<const uint8_t*>(tp[j0 + j]); });
 #pragma unroll
             for (int rr = 0; rr < RT; ++rr)
                 if (static_cast<uint32_t>(rr) < rows)
