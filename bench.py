@@ -125,7 +125,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    p.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS) + ["first_seen"],
+                   help="first_seen: only the first_seen_decode leg (cfg4's shape), for the counter runs")
+    p.add_argument("--no-first-seen", action="store_true",
+                   help="cfg2: skip the first_seen_decode leg (first-seen erasure patterns at cfg4's shape)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extra", action="store_true", help="skip the 1 MiB-stripe batched leg")
@@ -314,12 +317,29 @@ def device_tree_hash():
     return h.hexdigest()[:16]
 
 
+def _bsr_traced_name(printed):
+    """The library's matapply_bsr names -> the kernels' demangled names:
+    <RT> one-wave form, <RT,lds> LDS-phase form, <RT,lds,tbl> its table form,
+    <RT,ks,tbl> the input-split form (kernels.hip fill_bsr*)."""
+    if not printed.startswith("matapply_bsr<"):
+        return None
+    a = printed[len("matapply_bsr<"):-1].split(",")
+    rt = a[0]
+    form = ",".join(a[1:])
+    return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, zfec_hip::MatJob>" % rt,
+            "lds,tbl": "matapply_bsr<%s, true, zfec_hip::BsrTblJob>" % rt,
+            "ks,tbl": "matapply_bsr_ks<%s>" % rt}.get(form)
+
+
 def _same_kernel(traced, printed):
-    """rocprof's demangled name vs the library's name: the same name, or the
+    """rocprof's demangled name vs the library's name: the same name, the
     library's short template name as the leading arguments of the traced one
-    (matapply_reg<3,7> vs matapply_reg<3, 7, 3, true, true>)."""
-    if traced == printed:
+    (matapply_reg<3,7> vs matapply_reg<3, 7, 3, true, true>), or a
+    matapply_bsr form's name (_bsr_traced_name)."""
+    if traced == printed or traced == _bsr_traced_name(printed):
         return True
+    if printed.startswith("matapply_bsr<"):
+        return False
     if "<" not in traced or "<" not in printed or traced.split("<")[0] != printed.split("<")[0]:
         return False
     targs = [a.strip() for a in traced.split("<", 1)[1].rsplit(">", 1)[0].split(",")]
@@ -877,6 +897,88 @@ def run_batched_1mib(steps):
     return res
 
 
+FIRST_SEEN_PATTERNS = 5
+
+
+def run_first_seen(npat=FIRST_SEEN_PATTERNS):
+    """first_seen_decode leg: cfg4's shape (K=20/M=60, 1024 x 1 MiB stripes,
+    rows 256-byte aligned), decoded from `npat` erasure patterns the process
+    has never seen, each from 20 of the 40 parity blocks (every primary lost:
+    r = 20 rows recovered per stripe), with the JIT policy as shipped: no
+    compiled kernel exists for a first-seen matrix, so each runs on
+    matapply_bsr (zfec/fec.c:527-557 decodes every pattern on one path).
+    Beside it the same decode of the one pattern whose bit-sliced kernel is
+    compiled (parity blocks 40..59, fec_jit_prepare_decode).  Every launch is
+    one decode between HIP events after the received blocks are staged into
+    slot order (outside the events), one untimed launch of each kind first;
+    every result is checked against the data."""
+    k, m, ns = 20, 60, 1024
+    r = m - k
+    sz = -(-(1 << 20) // k)
+    ld = row_stride(sz)
+    gen = torch.Generator(device="cuda").manual_seed(2060)
+    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda", generator=gen)
+    par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
+    recv = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
+    out = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    stream = torch.cuda.current_stream()
+    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns,
+                      stream=stream.cuda_stream)
+    LEGS.add("first-seen setup", capi.last_kernel_name())
+    jit_slots = list(range(m - k, m))
+    code.jit_prepare_decode(jit_slots)  # loads (or compiles) the compiled kernel of this one pattern
+    rng = np.random.default_rng(5005)
+    seen = {tuple(jit_slots)}
+
+    def fresh_slots():
+        while True:
+            sl = tuple(sorted(int(x) for x in rng.choice(np.arange(k, m), size=k, replace=False)))
+            if sl not in seen:
+                seen.add(sl)
+                return list(sl)
+
+    def one(sl, leg):
+        for j, s in enumerate(sl):
+            recv[:, j].copy_(par[:, s - k])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        code.decode_batch(recv.data_ptr(), ld, k * ld, out.data_ptr(), ld, k * ld, sl, sz, ns,
+                          stream=stream.cuda_stream)
+        b.record(stream)
+        kern = capi.last_kernel_name()
+        LEGS.add(leg, kern)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :, :sz], data[:, :, :sz]), "first-seen decode != input"
+        return a.elapsed_time(b), kern
+
+    res = {"shape": "K=20/M=60, %d x 1 MiB stripes (sz %d, row stride %d), decode of all %d primaries from %d parity "
+                    "blocks" % (ns, sz, ld, k, k),
+           "algorithmic_bytes_per_launch": (k + k) * sz * ns, "patterns": npat}
+    hbm = lambda ms: (k + k) * sz * ns / (ms * 1e-3) / 1e9
+    for tag, pick, leg in (("first_seen", fresh_slots, "first-seen decode"),
+                           ("jit", lambda: jit_slots, "first-seen jit decode")):
+        one(pick(), leg + " (untimed)")
+        rows = [one(pick(), leg) for _ in range(npat)]
+        ms = [x for x, _ in rows]
+        kern = sorted(set(n for _, n in rows))
+        mean = float(np.mean(ms))
+        e = {"kernel": kern[0] if len(kern) == 1 else kern, "ms_mean": round(mean, 4),
+             "ms_min": round(float(np.min(ms)), 4), "ms_max": round(float(np.max(ms)), 4),
+             "hbm_GBps": round(hbm(mean), 1), "frac_of_peak": round(hbm(mean) / HBM_PEAK_GBPS, 4),
+             "input_GBps": round(k * sz * ns / (mean * 1e-3) / 1e9, 1)}
+        if len(kern) == 1:
+            e["valu_roofline"] = valu_roofline("first_seen", kern[0], mean)
+        res[tag] = e
+    res["first_seen_vs_jit"] = round(res["jit"]["ms_mean"] / res["first_seen"]["ms_mean"], 4)
+    res["timing"] = ("one decode launch per pattern between HIP events (staging copies outside), JIT mode as "
+                     "shipped (auto): a first-seen matrix has no compiled kernel; one untimed launch of each kind "
+                     "first")
+    del data, par, recv, out
+    torch.cuda.empty_cache()
+    return res
+
+
 def dry_run(args):
     """--dry-run: the ranks and their process group, no GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -899,6 +1001,15 @@ def main():
     if args.dry_run:
         return dry_run(args)
     dist, rank, world = dist_setup(args.gpus)
+    if args.workload == "first_seen":
+        if world != 1:
+            raise SystemExit("--workload first_seen runs on one GPU")
+        fs = run_first_seen()
+        if args.legs_out:
+            with open(args.legs_out, "w") as f:
+                json.dump({"workload": "first_seen", "legs": LEGS.runs}, f)
+        print(json.dumps({"first_seen_decode": fs}), flush=True)
+        return
     ranks_seen = dist.get_world_size() if dist is not None else 1
     if ranks_seen != args.gpus:
         raise SystemExit("bench.py: the process group has %d ranks, --gpus %d" % (ranks_seen, args.gpus))
@@ -1004,6 +1115,8 @@ def main():
         out["decode_fresh_pattern"] = t["decode_fresh"]
     if rank == 0 and not args.no_extra and args.workload == "cfg2":
         out["batched_1MiB"] = run_batched_1mib(20)
+    if rank == 0 and not args.no_first_seen and args.workload == "cfg2":
+        out["first_seen_decode"] = run_first_seen()
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             csz = min(sz, -(-(64 << 20) // k))  # sample stripes of at most 64 MiB (same K/M)

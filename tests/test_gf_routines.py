@@ -75,3 +75,31 @@ def test_every_routine_multiplies():
                 v[d] = v[s0] ^ val(s1) ^ val(s2)
             want = _planes(acc0 ^ mul[c][x])
             assert [v[ACC + b] for b in range(8)] == want, (c, trial)
+
+
+def test_every_call_statement_restores_m0():
+    """s_set_gpr_idx_on writes M0, which hipcc treats as reserved (an "m0"
+    clobber is ignored: cdna_hip_programming.md, "Operands and clobbers"), so
+    each bsr_input<RT> statement must save M0 into an early-clobber SGPR before
+    its first index-mode call and restore it after its last one."""
+    text = open(INC).read()
+    bodies = re.findall(r"void bsr_input<(\d+)>\(.*?asm volatile\((.*?)\);\n\}", text, re.S)
+    assert [int(rt) for rt, _ in bodies] == list(range(1, 11))
+    for rt, body in bodies:
+        ins = [s for s in re.findall(r'"([^"]*)"', body.split("\n        :")[0])]
+        ins = [ln.replace("\\n\\t", "") for ln in ins]
+        save = [i for i, ln in enumerate(ins) if re.fullmatch(r"s_mov_b32 %(\d+), m0", ln)]
+        restore = [i for i, ln in enumerate(ins) if re.fullmatch(r"s_mov_b32 m0, %(\d+)", ln)]
+        idx_on = [i for i, ln in enumerate(ins) if ln.startswith("s_set_gpr_idx_on")]
+        assert len(idx_on) == int(rt), rt
+        assert len(save) == 1 and len(restore) == 1, rt
+        assert save[0] < idx_on[0] and restore[0] > idx_on[-1], rt
+        # no instruction after the restore writes M0, and the save and restore
+        # name the same operand, which is an early-clobber SGPR output
+        assert not any("m0" in ln or "gpr_idx_on" in ln for ln in ins[restore[0] + 1:]), rt
+        n_save = re.fullmatch(r"s_mov_b32 %(\d+), m0", ins[save[0]]).group(1)
+        n_rest = re.fullmatch(r"s_mov_b32 m0, %(\d+)", ins[restore[0]]).group(1)
+        assert n_save == n_rest, rt
+        outs = body.split("\n        :")[1]
+        operands = re.findall(r'"([^"]+)"\(', outs)
+        assert operands[int(n_save)] == "=&s", (rt, operands[int(n_save)])

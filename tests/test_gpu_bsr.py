@@ -373,3 +373,45 @@ def test_bsr_table_form_batched_guards(bsr_only):
     assert (o[:, :, sz:] == 0xA5).all(), "write past a row"
     for s_ in range(ns):
         assert (o[s_, :, :sz] == oracle.encode(k, m, data[s_])).all(), s_
+
+
+# Launches past the grid cap (kernels.hip launch_bsr / launch_bsr_wide: at most
+# CUs x 1024 workgroups, 262,144 on MI355X) walk their units grid-stride; these
+# shapes give each form more units than that: the one-wave form (5/13:
+# matapply_bsr<8>), the LDS-phase form (6/20: two tiles of 7) and the ks form
+# (33/34: one row, inputs split over the waves).
+@pytest.mark.parametrize("k,m,sz,ns", [(5, 13, 2048, 300000), (6, 20, 2048, 270000), (33, 34, 4096, 132000)])
+def test_bsr_past_grid_cap(bsr_only, k, m, sz, ns):
+    r = m - k
+    units = ns * (sz // 2048)
+    assert units > 256 * 1024
+    g = torch.Generator(device="cuda").manual_seed(k * m)
+    data = torch.randint(0, 256, (ns, k, sz), dtype=torch.uint8, device="cuda", generator=g)
+    par = torch.full((ns, r, sz), 0xA5, dtype=torch.uint8, device="cuda")
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    code.encode_batch(data.data_ptr(), sz, k * sz, par.data_ptr(), sz, r * sz, list(range(k, m)), sz, ns, stream=st)
+    torch.cuda.synchronize()
+    name = capi.last_kernel_name()
+    want = "matapply_bsr<%d,ks,tbl>" % r if k > 32 else bsr_name(r, units)
+    assert name == want or (k <= 32 and is_bsr(name, r, units)), name
+    # decode from the last k blocks (all the parity there is, plus the highest
+    # primaries): recovered blocks must equal the data in every stripe
+    nums = list(range(m - k, m))
+    sl = place(nums, k)
+    miss = [i for i in range(k) if sl[i] >= k]
+    allb = torch.cat([data, par], dim=1)
+    rv = allb[:, sl, :].contiguous()
+    del allb
+    rec = torch.full((ns, len(miss), sz), 0x5A, dtype=torch.uint8, device="cuda")
+    code.decode_batch(rv.data_ptr(), sz, k * sz, rec.data_ptr(), sz, len(miss) * sz, sl, sz, ns, stream=st)
+    torch.cuda.synchronize()
+    assert bool(torch.equal(rec, data[:, miss, :])), "a stripe was not recovered"
+    rng = np.random.default_rng(ns)
+    # stripes on both sides of the first grid-stride step, the last one, random ones
+    cap = 256 * 1024 * 2048 // sz
+    for s in sorted({0, cap - 1, cap, ns - 1} | set(int(x) for x in rng.integers(0, ns, size=12))):
+        got = par[s].cpu().numpy()
+        assert (got == oracle.encode(k, m, data[s].cpu().numpy())).all(), s
+        want_rec = oracle.decode(k, m, rv[s].cpu().numpy(), sl)
+        assert (rec[s].cpu().numpy() == want_rec).all(), s

@@ -776,19 +776,23 @@ def test_config2_64mib_vs_oracle():
 class _kernels(object):
     """Which kernel family serves a full-size launch: "jit" = the run-time
     specialised bit-sliced kernel of the launch's matrix (compiled up front with
-    fec_jit_prepare_*, as bench.py times it), "generic" = matapply_bsg (the
-    bit-sliced kernel with the matrix as run-time data: what a first-seen
-    erasure pattern runs on), "table" = the table-lookup kernels (JIT and
-    generic kernel off).  check(what) asserts the last launch's kernel."""
+    fec_jit_prepare_*, as bench.py times it), "bsr" = matapply_bsr (the
+    bit-sliced kernel with the matrix as run-time data, one precompiled routine
+    call per coefficient: the default for a first launch of a matrix and for
+    every first-seen erasure pattern, generic mode 2), "generic" = matapply_bsg
+    (the same with the combination choice as LDS reads, generic mode 1),
+    "table" = the table-lookup kernels (JIT and generic kernels off).
+    check(what) asserts the last launch's kernel."""
 
-    PREFIX = {"jit": "zfec_hip_bitslice", "generic": "matapply_bsg", "table": "matapply_lds"}
+    PREFIX = {"jit": "zfec_hip_bitslice", "bsr": "matapply_bsr", "generic": "matapply_bsg", "table": "matapply_lds"}
+    GENERIC = {"jit": 2, "bsr": 2, "generic": 1, "table": 0}
 
     def __init__(self, kind):
         self.kind = kind
 
     def __enter__(self):
         self.prev = capi.jit_mode(capi.JIT_AUTO if self.kind == "jit" else capi.JIT_OFF)
-        self.prev_g = capi.generic_mode(0 if self.kind == "table" else 1)
+        self.prev_g = capi.generic_mode(self.GENERIC[self.kind])
         return self
 
     def __exit__(self, *exc):
@@ -850,11 +854,12 @@ def _batched_full_size(k, m, S, ns, seed, sample, kernels=None):
         assert (rv == oracle.decode(k, m, recv[s, :, :sz].cpu().numpy(), slots)).all(), s
 
 
-@pytest.mark.parametrize("kind", ["jit", "generic", "table"])
+@pytest.mark.parametrize("kind", ["jit", "bsr", "generic", "table"])
 def test_config4_1024_stripes_of_1mib(kind):
     """cfg4: K=20/M=60, 1024 x 1 MiB stripes in one launch, on the kernel
-    bench.py times (the bit-sliced kernel of the matrix), on the generic
-    bit-sliced kernel and on the table kernel."""
+    bench.py times (the bit-sliced kernel of the matrix), on matapply_bsr (what
+    the first launch of the matrix and every first-seen decode run on), on
+    matapply_bsg and on the table kernel."""
     with _kernels(kind) as kn:
         _batched_full_size(20, 60, 1 << 20, 1024, 4, sample=6, kernels=kn)
 
@@ -864,13 +869,14 @@ def test_config5_1e6_objects_of_4kib():
     _batched_full_size(3, 10, 4096, 10 ** 6, 5, sample=200)
 
 
-@pytest.mark.parametrize("kind", ["jit", "generic", "table"])
+@pytest.mark.parametrize("kind", ["jit", "bsr", "generic", "table"])
 def test_config3_256mib_roundtrip(kind):
     """K=10/M=16, 256 MiB: encode, drop primaries 0-5, decode; compare by
     equality on the device (size-independent property) and check parity rows
     and recovered blocks against the oracle on slices at the start, middle and
-    end (column independence), on the kernel bench.py times, on the generic
-    bit-sliced kernel and on the table kernel."""
+    end (column independence), on the kernel bench.py times, on matapply_bsr
+    (the first-launch default: matapply_bsr_solo<6> here), on matapply_bsg and
+    on the table kernel."""
     k, m, S = 10, 16, 256 << 20
     sz = -(-S // k)
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -1337,7 +1343,9 @@ def test_batch_call_and_ctypes_paths_agree():
 @pytest.mark.parametrize("mode", ["signal", "sync"])
 def test_medium_call_wait_modes(mode, knobs):
     """Synchronous calls from bytes too large for one workgroup: on the
-    zero-copy path (at most 256 KiB of host blocks, k <= 4) the stream writes
+    zero-copy path (the kernel reads and writes the pinned bounce buffer in
+    place: up to 1.5 MiB of host blocks for the register shapes k <= 4, r <= 8,
+    up to 256 KiB for wider codes; fec_abi.cpp run_single) the stream writes
     the call's sequence number into the pinned completion word after the
     kernel (hipStreamWriteValue32) and the caller spins on it; the copy path
     and ZFEC_HIP_WAIT=sync wait in hipStreamSynchronize.  Bit-exact against

@@ -2,12 +2,14 @@
 """A/B of the three kernel families that can serve a wide-code launch, on
 device-resident stripes (interleaved rounds, medians):
 
-  table   matapply_lds (v_perm table lookups; JIT off, generic off)
-  bsg     matapply_bsg<RT,2,nosb> (bit-sliced, coefficients as run-time data)
-  bsg_sb  matapply_bsg<RT,2> (a scheduling barrier after each row; ZFEC_HIP_BSG_SB=1)
-  bsg_bb  matapply_bsg<RT,2,bb> (input build balanced over the 4 waves; ZFEC_HIP_BSG_BB=1)
-  bsg_p4  matapply_bsg<RT,4> (4 inputs per LDS phase; ZFEC_HIP_BSG_PHASE=4)
+  table   matapply_lds (v_perm table lookups; JIT off, generic mode 0)
+  bsg     matapply_bsg<RT,2> (bit-sliced, coefficients as run-time data; generic mode 1)
+  bsr     matapply_bsr (bit-sliced, one precompiled routine call per coefficient; generic mode 2)
   jit     zfec_hip_bitslice_* (bit-sliced, the matrix compiled in; hipRTC)
+
+(Round 2's bsg_sb / bsg_bb / bsg_p4 variants and the knobs that selected them
+were removed with the code in round 4; profiles/r02_bsg_ab*.log keeps their
+figures.)
 
 Shapes: cfg3 (K=10/M=16, one 256 MiB stripe) and cfg4 (K=20/M=60, 1024 x
 1 MiB stripes), encode and last-k decode.  Then decode_fresh: cfg4 decodes,
@@ -35,10 +37,8 @@ sys.path.insert(0, ROOT)
 from zfec_amd import capi  # noqa: E402
 
 SHAPES = {"cfg3": (10, 16, 256 << 20, 1), "cfg4": (20, 60, 1 << 20, 1024)}
-VARIANTS = [("table", capi.JIT_OFF, 0, {}), ("bsg", capi.JIT_OFF, 1, {}),
-            ("bsg_p4", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_PHASE": "4"}),
-            ("bsg_sb", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_SB": "1"}),
-            ("bsg_bb", capi.JIT_OFF, 1, {"ZFEC_HIP_BSG_BB": "1"}), ("jit", capi.JIT_FORCE, 1, {})]
+VARIANTS = [("table", capi.JIT_OFF, 0), ("bsg", capi.JIT_OFF, 1), ("bsr", capi.JIT_OFF, 2),
+            ("jit", capi.JIT_FORCE, 2)]
 
 
 def place(nums, k):
@@ -50,11 +50,7 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-def set_variant(jit, gen, env):
-    os.environ.pop("ZFEC_HIP_BSG_PHASE", None)
-    os.environ.pop("ZFEC_HIP_BSG_SB", None)
-    os.environ.pop("ZFEC_HIP_BSG_BB", None)
-    os.environ.update(env)
+def set_variant(jit, gen):
     capi.jit_mode(jit)
     capi.generic_mode(gen)
 
@@ -84,8 +80,8 @@ def main():
         times = {(v[0], d): [] for v in VARIANTS for d in ("enc", "dec")}
         kern = {}
         for rnd in range(args.rounds):
-            for name, jit, gen, env in VARIANTS:
-                set_variant(jit, gen, env)
+            for name, jit, gen in VARIANTS:
+                set_variant(jit, gen)
                 out, rec = outs[name], recs[name]
 
                 def enc():
@@ -115,7 +111,7 @@ def main():
                     times[(name, d)].append(e0.elapsed_time(e1) / args.reps)
         base = outs["table"][:, :, :sz]
         missing = [i for i in range(k) if slots[i] >= k]
-        for name, _, _, _ in VARIANTS:
+        for name, _, _ in VARIANTS:
             ok_enc = bool(torch.equal(outs[name][:, :, :sz], base))
             ok_dec = bool(torch.equal(recs[name][:, :, :sz], data[:, missing, :sz]))
             for d, nb in (("enc", k + r), ("dec", k + nrec)):
@@ -129,7 +125,8 @@ def main():
         if shape == "cfg4" and args.fresh:
             allb = torch.cat([data, outs["table"]], dim=1)  # [ns, m, ld]
             rng = np.random.default_rng(99)
-            ms_b, ms_t, names, ok = [], [], set(), True
+            ms_b, ms_t, ms_r, names, ok = [], [], [], {"bsg": set(), "bsr": set()}, True
+            out_r = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
             out_b = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
             out_t = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
             for p in range(args.fresh):
@@ -139,29 +136,30 @@ def main():
                 if nr == 0:
                     continue
                 rv = allb[:, sl, :].contiguous()
-                for name, tgt, lst in (("bsg", out_b, ms_b), ("table", out_t, ms_t)):
-                    set_variant(capi.JIT_OFF, 1 if name == "bsg" else 0, {})
+                for name, tgt, lst in (("bsr", out_r, ms_r), ("bsg", out_b, ms_b), ("table", out_t, ms_t)):
+                    set_variant(capi.JIT_OFF, {"bsr": 2, "bsg": 1, "table": 0}[name])
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
                     code.decode_batch(rv.data_ptr(), ld, k * ld, tgt.data_ptr(), ld, k * ld, sl, sz, ns,
                                       stream=st.cuda_stream)
                     e1.record(st)
-                    if name == "bsg":
-                        names.add(capi.last_kernel_name())
+                    if name in names:
+                        names[name].add(capi.last_kernel_name())
                     torch.cuda.synchronize()
                     lst.append((e0.elapsed_time(e1), nr))
                 miss = [i for i in range(k) if sl[i] >= k]
                 ok = ok and bool(torch.equal(out_b[:, :nr, :sz], out_t[:, :nr, :sz]))
+                ok = ok and bool(torch.equal(out_r[:, :nr, :sz], out_t[:, :nr, :sz]))
                 ok = ok and bool(torch.equal(out_b[:, :nr, :sz], data[:, miss, :sz]))
-            for name, lst in (("bsg", ms_b), ("table", ms_t)):
+            for name, lst in (("bsr", ms_r), ("bsg", ms_b), ("table", ms_t)):
                 gbps = [k * sz * ns / (t * 1e-3) / 1e9 for t, _ in lst]
                 row = {"patterns": len(lst), "mean_recovered": round(float(np.mean([n for _, n in lst])), 1),
                        "input_GBps_mean": round(float(np.mean(gbps)), 1),
                        "input_GBps_min": round(float(np.min(gbps)), 1),
-                       "kernels": sorted(names) if name == "bsg" else "table", "bitexact": ok}
+                       "kernels": sorted(names[name]) if name in names else "table", "bitexact": ok}
                 res["cfg4 decode_fresh %s" % name] = row
                 print("cfg4 decode_fresh", "%-6s" % name, json.dumps(row), flush=True)
-    set_variant(capi.JIT_AUTO, 1, {})
+    set_variant(capi.JIT_AUTO, 2)
     print(json.dumps(res))
 
 

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Compile (hipRTC, no GPU needed) the bit-sliced kernels the GPU tests and the
 bench workloads launch, into zfec_amd/jit_cache/ next to libzfec_hip.so, so a
-fresh GPU box loads them instead of compiling.  The ZFEC_HIP_JIT_* knobs in the
-environment select the variant (tools/jit_bench.py sets them per variant)."""
+fresh GPU box loads them instead of compiling."""
 import os
 import sys
 import time

@@ -375,7 +375,7 @@ def reuse_host_memory(keep_bytes=1 << 30, mmap_threshold=32 << 20):
     trims on free), so every call faults them in and every free returns them to
     the kernel.  On the MI355X host that is most of a K=3/M=10 64 MiB encode from
     ``bytes``: 3.0 GB/s per call with the freeing counted, 15.5 GB/s when blocks
-    are reused (tools/stage_probe.py).  This sets
+    are reused (tools/e2e_host.py).  This sets
     M_MMAP_THRESHOLD (blocks under ``mmap_threshold`` come from the heap; glibc
     caps it at 32 MiB) and M_TRIM_THRESHOLD (up to ``keep_bytes`` of free heap is
     kept), the same as ``GLIBC_TUNABLES=glibc.malloc.mmap_threshold=...:

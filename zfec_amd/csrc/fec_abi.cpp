@@ -825,7 +825,8 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // kZcWideLimit: K=20/M=60 from bytes, 4 KiB stripes encode in 20.5 us in
     // place against 25.3 us with the copies, 64 KiB (197 KB of host blocks)
     // 44.7 against 47.9 us, but 128 KiB (393 KB) 63.8 against 57.9 us
-    // (tools/small_ab_inproc.py --set zcwide, profiles/r03_zcwide_ab.log).
+    // (round-3 A/B, profiles/r03_zcwide_ab.log).  Fixed since round 4; the
+    // GPU test test_medium_call_wait_modes runs K=10/M=16 on both sides of it.
     constexpr size_t kZcWideLimit = size_t(256) << 10;
     const bool zc_kernel = (k <= 4 && r <= 8) || sz * nhost <= kZcWideLimit;
     bool signalled = false;
@@ -1415,12 +1416,13 @@ FEC_API int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* st
     if (!gpu_available()) return set_status(FEC_ENODEV, "no GPU visible to HIP (the engine has no CPU path)");
     return guarded([&] {
         const unsigned call = flags & (FEC_FLAG_ASYNC | FEC_FLAG_LIBRARY_STREAM);
-        int devs[64];
-        size_t ndevs = 0;
+        // every device a job ran on, each once (no cap: a synchronous call
+        // must wait on all of them before it reports FEC_OK)
+        std::vector<int> devs;
         auto note_dev = [&](int dev) {
-            for (size_t q = 0; q < ndevs; ++q)
-                if (devs[q] == dev) return;
-            if (ndevs < 64) devs[ndevs++] = dev;
+            for (int d : devs)
+                if (d == dev) return;
+            devs.push_back(dev);
         };
         size_t i = 0;
         while (i < njobs) {
@@ -1469,16 +1471,16 @@ FEC_API int fec_run_batch_jobs(const fec_batch_job* jobs, size_t njobs, void* st
                 if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
             } else if (!(flags & FEC_FLAG_LIBRARY_STREAM)) {
                 // the null stream: each job ran on its own device's null stream
-                for (size_t q = 0; q < ndevs; ++q) {
-                    DeviceGuard guard(devs[q]);
+                for (int dv : devs) {
+                    DeviceGuard guard(dv);
                     const hipError_t e = hipStreamSynchronize(nullptr);
                     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
                 }
             } else {
-                for (size_t q = 0; q < ndevs; ++q) {
-                    DeviceGuard guard(devs[q]);
+                for (int dv : devs) {
+                    DeviceGuard guard(dv);
                     DevCtx* d = nullptr;
-                    if (dev_ctx(devs[q], &d)) return t_status;
+                    if (dev_ctx(dv, &d)) return t_status;
                     const hipError_t e = hipStreamSynchronize(d->stream);
                     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
                 }
