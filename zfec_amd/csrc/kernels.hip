@@ -1156,7 +1156,7 @@ struct alignas(16) BsrTblJob {
 };
 
 template <int RT, bool TBL, class J>
-__global__ __launch_bounds__(512) void matapply_bsr(const J job) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void matapply_bsr(const J job) {
     constexpr uint32_t RTP = bsr_rtp<RT>();
     extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
     const uint32_t lane = threadIdx.x & 63u;
@@ -1164,6 +1164,7 @@ __global__ __launch_bounds__(512) void matapply_bsr(const J job) {
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
     constexpr uint32_t kp = kBsrPhase;
+    constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
     // block pointers and coefficients: kernel arguments (MatJob) or the
     // device-side table (BsrTblJob: k input and r output pointers, then per
     // row group and wave [input][RTP] coefficient bytes); the walk's "stripes"
@@ -1213,10 +1214,10 @@ __global__ __launch_bounds__(512) void matapply_bsr(const J job) {
         for (uint32_t ph = 0; ph < k; ph += kp) {
             const uint32_t kn = k - ph < kp ? k - ph : kp;
             // inputs -> bit-planes -> LDS, inputs wave, wave + nw, ... in batches
-            for (uint32_t j0 = wave; j0 < kn; j0 += kBsrBatch * nw) {
-                u32x4 x[kBsrBatch][2];
+            for (uint32_t j0 = wave; j0 < kn; j0 += kBat * nw) {
+                u32x4 x[kBat][2];
 #pragma unroll
-                for (int q = 0; q < kBsrBatch; ++q) {
+                for (int q = 0; q < kBat; ++q) {
                     const uint32_t j = j0 + q * nw;
                     if (j < kn) {  // wave-uniform
                         const uint8_t* ip = in_ptr(ph + j) + ib;
@@ -1225,7 +1226,7 @@ __global__ __launch_bounds__(512) void matapply_bsr(const J job) {
                     }
                 }
 #pragma unroll
-                for (int q = 0; q < kBsrBatch; ++q) {
+                for (int q = 0; q < kBat; ++q) {
                     const uint32_t j = j0 + q * nw;
                     if (j < kn) {
                         uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
