@@ -6,6 +6,7 @@ routines matapply_bsr calls (one per coefficient):
   bit-planes of random bytes -- after the combination XORs that bsr_input emits
   -- adds exactly c * x (the oracle's gf_mul, zfec/fec.c:58-86 via
   oracle/fec_oracle.c) to the accumulator row;
+- the "set" twins (256 + c) write c * x over the row;
 - every routine fits its 72-byte slot (the .org directives would fail the
   build otherwise; this names the routine)."""
 
@@ -35,7 +36,7 @@ def _parse():
     routines = {}
     for m in re.finditer(r'"\.org zfec_gf_routines \+ (\d+)\\n"\s*\n\s*"([^"]*)"', body):
         routines[int(m.group(1))] = m.group(2).split("\\n")
-    combos = re.search(r"bsr_input<1>.*?asm volatile\((.*?)s_getpc", text, re.S).group(1)
+    combos = re.search(r"bsr_input<1>.*?asm volatile\((.*?)s_set_gpr_idx_on", text, re.S).group(1)
     xors = re.findall(r"v_xor_b32 v(\d+), v(\d+), v(\d+)", combos)
     return routines, [(int(a), int(b), int(c)) for a, b, c in xors]
 
@@ -46,16 +47,21 @@ def _planes(x):
 
 
 def test_every_routine_multiplies():
+    """Routines 0-255 add c * x to the row; 256-511 (the "set" twins a wave's
+    first input calls) write c * x over whatever the row held."""
     routines, xors = _parse()
-    assert len(routines) == 256 and len(xors) == 22
+    assert len(routines) == 512 and len(xors) == 22
     rng = np.random.default_rng(72)
     mul = np.array([[oracle.gf_mul(a, b) for b in range(256)] for a in range(256)], dtype=np.uint8)
-    op = re.compile(r"v_bitop3_b32 v(\d+), v(\d+), (v\d+|0), (v\d+|0) bitop3:0x96")
-    for c in range(256):
-        lines = routines[72 * c]
-        assert lines[-2] == "s_setpc_b64 s[30:31]" and lines[-1] == "", (c, lines[-2:])
+    op = re.compile(r"v_bitop3_b32 v(\d+), v(\d+), (v\d+|0), (v\d+|0) bitop3:(0x96|0x66)")
+    for slot in range(512):
+        c, first = slot % 256, slot >= 256
+        lines = routines[72 * slot]
+        assert lines[-2] == "s_setpc_b64 s[30:31]" and lines[-1] == "", (slot, lines[-2:])
         body = lines[:-2]
-        assert 8 * len(body) + 4 <= 72, c
+        assert 8 * len(body) + 4 <= 72, slot
+        if first:  # every plane written
+            assert sorted(int(op.fullmatch(ln).group(1)) for ln in body) == list(range(ACC, ACC + 8)), slot
         for trial in range(3):
             x = rng.integers(0, 256, size=32, dtype=np.uint8)
             acc0 = rng.integers(0, 256, size=32, dtype=np.uint8)
@@ -68,13 +74,14 @@ def test_every_routine_multiplies():
                 v[ACC + b] = pl
             for ln in body:
                 m = op.fullmatch(ln)
-                assert m, (c, ln)
-                d, s0, s1, s2 = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)
-                assert d == s0 and ACC <= d < ACC + 8, (c, ln)
+                assert m, (slot, ln)
+                d, s0, s1, s2, tt = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4), m.group(5)
+                assert d == s0 and ACC <= d < ACC + 8, (slot, ln)
+                assert tt == ("0x66" if first else "0x96"), (slot, ln)
                 val = lambda s: 0 if s == "0" else v[int(s[1:])]
-                v[d] = v[s0] ^ val(s1) ^ val(s2)
-            want = _planes(acc0 ^ mul[c][x])
-            assert [v[ACC + b] for b in range(8)] == want, (c, trial)
+                v[d] = (0 if first else v[s0]) ^ val(s1) ^ val(s2)
+            want = _planes(mul[c][x] if first else acc0 ^ mul[c][x])
+            assert [v[ACC + b] for b in range(8)] == want, (slot, trial)
 
 
 def test_every_call_statement_restores_m0():
@@ -91,9 +98,16 @@ def test_every_call_statement_restores_m0():
         save = [i for i, ln in enumerate(ins) if re.fullmatch(r"s_mov_b32 %(\d+), m0", ln)]
         restore = [i for i, ln in enumerate(ins) if re.fullmatch(r"s_mov_b32 m0, %(\d+)", ln)]
         idx_on = [i for i, ln in enumerate(ins) if ln.startswith("s_set_gpr_idx_on")]
-        assert len(idx_on) == int(rt), rt
+        idx_idx = [i for i, ln in enumerate(ins) if ln.startswith("s_set_gpr_idx_idx")]
+        idx_off = [i for i, ln in enumerate(ins) if ln.startswith("s_set_gpr_idx_off")]
+        calls = [i for i, ln in enumerate(ins) if ln.startswith("s_swappc_b64")]
+        # index mode on once, moved to row rr (8 rr) before each later call, off after the last
+        assert len(idx_on) == 1 and len(idx_off) == 1 and len(calls) == int(rt), rt
+        assert [ins[i] for i in idx_idx] == ["s_set_gpr_idx_idx %d" % (8 * rr) for rr in range(1, int(rt))], rt
+        assert idx_on[0] < calls[0] and calls[-1] < idx_off[0], rt
+        assert all(calls[rr - 1] < idx_idx[rr - 1] < calls[rr] for rr in range(1, int(rt))), rt
         assert len(save) == 1 and len(restore) == 1, rt
-        assert save[0] < idx_on[0] and restore[0] > idx_on[-1], rt
+        assert save[0] < idx_on[0] and restore[0] > idx_off[0], rt
         # no instruction after the restore writes M0, and the save and restore
         # name the same operand, which is an early-clobber SGPR output
         assert not any("m0" in ln or "gpr_idx_on" in ln for ln in ins[restore[0] + 1:]), rt

@@ -14,4 +14,5 @@ mkdir -p $OUT
 ARGS="--workload $W --steps 3 --warmup 1 --no-cpu --no-extra $*"
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS --output-format csv -d $OUT/sq -o sq -- python3 $ROOT/bench.py $ARGS > $OUT/sq.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/lds -o lds -- python3 $ROOT/bench.py $ARGS > $OUT/lds.log 2>&1
+timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_SALU SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_IFETCH SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sca -o sca -- python3 $ROOT/bench.py $ARGS > $OUT/sca.log 2>&1
 echo pmc-sq-done $W

@@ -26,7 +26,7 @@ def summarize(tag, workloads):
            "workloads": {}}
     for w in workloads:
         ws = {}
-        for sub in ("ic", "sq", "lds"):
+        for sub in ("ic", "sq", "lds", "sca"):
             files = glob.glob(os.path.join(ROOT, "gpurun_out", tag, w, sub, "**", "*counter_collection.csv"),
                               recursive=True)
             if not files:

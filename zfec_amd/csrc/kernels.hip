@@ -54,6 +54,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 #include <utility>
 
 namespace zfec_hip {
@@ -1121,7 +1122,7 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 //
 // Unit = 2 KiB of every block of a stripe (32 bytes per lane, like the JIT
 // kernels); rows in tiles of <= RT <= 10 (the accumulators of a tile live in
-// v54..v53+8RT).  Two forms:
+// v38..v37+8RT, gf_routines.inc).  Two forms:
 //   matapply_bsr_solo<RT> (one tile, r <= 10): one wave per unit, no LDS; the
 //       wave loads and transposes its inputs two ahead;
 //   matapply_bsr<RT> ("lds", r > 10): one workgroup per unit, a wave per
@@ -1130,34 +1131,77 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 //       tile.  All k inputs in LDS at once (k * 2 KiB) capped the workgroups
 //       per CU and measured 0.51 ms against 0.37-0.38 with phases of 8 on
 //       cfg4's first-seen decodes (profiles/r04_bsr_ab.json).
-// Coefficients: MatJob::coef as [tile][input][RTP] bytes (RTP = RT rounded up
-// to 4, rows past the tile 0: routine 0 only returns).
+// Coefficients: absolute routine addresses (BsrJob / BsrTblJob below).
 // ---------------------------------------------------------------------------
 #include "gf_routines.inc"
 
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
 constexpr int kBsrBatch = 4;          // inputs a wave loads at once
 constexpr uint32_t kBsrPhase = 8;     // inputs whose planes share LDS at a time (multi-wave form)
+constexpr int kBsrMaxOut = 4 * kBsrMaxRows;  // rows of the kernel-argument form (4 tiles)
+constexpr int kBsrArgAddrs = 432;     // routine addresses the kernel-argument form holds
 
-template <int RT>
-__host__ __device__ constexpr uint32_t bsr_rtp() {
-    return (RT + 3) / 4 * 4;
-}
+// Routine addresses: every coefficient reaches the kernel as the absolute
+// address of its routine (zfec_gf_routines + 72 c on the launch's device,
+// bsr_routine_base), in the kernel's walk order [group][wave][input][row],
+// RT per (wave, input) -- rows past a wave's tile hold routine 0's address,
+// which only returns.  Kernel-argument form (k <= 32, r <= 40, at most
+// kBsrArgAddrs addresses): block pointers and addresses in the arguments.
+struct alignas(16) BsrJob {
+    uint64_t sz, in_sstride, out_sstride;
+    uint32_t nstripes, k, r, cps, gs_c, gs_s;
+    uint32_t nt;  // one-wave form: row tiles per unit
+    uint32_t pad_;
+    const uint8_t* in[kMaxIn];
+    uint8_t* out[kBsrMaxOut];
+    uint64_t addr[kBsrArgAddrs];
+};
+static_assert(sizeof(BsrJob) <= 4096, "kernel arguments are limited to 4 KiB");
 
-// Block pointers and coefficients of a table-form matapply_bsr launch
-// (k > 32 or more rows than one workgroup's tiles hold): a device-side table
-// the host fills per launch (TableRing), read with scalar loads.
+// Table form (k > 32, or more addresses than the arguments hold): the block
+// pointers in the arguments, the addresses in a device-side table the host
+// uploads once per matrix and layout and keeps (bsr_addr_table), read with
+// scalar loads.
+constexpr int kBsrTblPtrs = 320;  // k + r block pointers of a table-form launch
 struct alignas(16) BsrTblJob {
     uint64_t sz, in_sstride, out_sstride;
     uint32_t nstripes, k, r, cps, gs_c, gs_s;
-    uint32_t ngroups;  // row groups (LDS form): workgroup units are (group, stripe, unit) triples
+    uint32_t ngroups;  // row groups: workgroup units are (group, stripe, unit) triples
     uint32_t pad_;
-    const uint8_t* table;
+    const uint64_t* addr;             // device: [group][wave][input][RT] routine addresses
+    const uint8_t* ptr[kBsrTblPtrs];  // k input block pointers, then r output block pointers
 };
+static_assert(sizeof(BsrTblJob) <= 4096, "kernel arguments are limited to 4 KiB");
+
+// Reads input j's RT routine addresses (scalar loads).
+// (The row offset is added to a 64-bit pointer, so the loads share one
+// address and merge into s_load_dwordx16 / x4 with immediate offsets.)
+template <int RT>
+__device__ __forceinline__ void bsr_addrs(uint64_t (&ad)[RT], CU64 ca, uint32_t j) {
+    const CU64 q = ca + static_cast<uint64_t>(j) * RT;
+#pragma unroll
+    for (int rr = 0; rr < RT; ++rr) ad[rr] = q[rr];
+}
+
+// The address of zfec_gf_routines on this device, computed the way a call
+// site would (s_getpc + the rel32 relocation) and stored by lane 0 with a
+// vector store; the host reads it once per device (bsr_routine_base).
+__global__ void bsr_table_probe(uint64_t* out) {
+    uint32_t lo, hi;
+    asm volatile(
+        "s_getpc_b64 s[26:27]\n\t"
+        "s_add_u32 s26, s26, zfec_gf_routines@rel32@lo+4\n\t"
+        "s_addc_u32 s27, s27, zfec_gf_routines@rel32@hi+12\n\t"
+        "s_mov_b32 %0, s26\n\t"
+        "s_mov_b32 %1, s27"
+        : "=s"(lo), "=s"(hi)
+        :
+        : "s26", "s27", "scc");
+    if (threadIdx.x == 0) out[0] = (static_cast<uint64_t>(hi) << 32) | lo;
+}
 
 template <int RT, bool TBL, class J>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void matapply_bsr(const J job) {
-    constexpr uint32_t RTP = bsr_rtp<RT>();
     extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1165,52 +1209,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
     const uint32_t k = job.k, r = job.r;
     constexpr uint32_t kp = kBsrPhase;
     constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
-    // block pointers and coefficients: kernel arguments (MatJob) or the
-    // device-side table (BsrTblJob: k input and r output pointers, then per
-    // row group and wave [input][RTP] coefficient bytes); the walk's "stripes"
-    // are (row group, stripe) pairs, group-major
+    // block pointers and routine addresses: kernel arguments (BsrJob) or the
+    // device-side table (BsrTblJob); the walk's "stripes" are (row group,
+    // stripe) pairs, group-major
     const uint32_t ns = job.nstripes;
     uint32_t ng = 1;
-    CU64 tp = nullptr;
-    KPtr<MatJob> kj = nullptr;
-    if constexpr (TBL) {
-        ng = job.ngroups;
-        tp = (CU64)job.table;
-    } else {
-        kj = kernarg_job<MatJob>();
-    }
+    KPtr<J> kj = kernarg_job<J>();
+    if constexpr (TBL) ng = job.ngroups;
     auto in_ptr = [&](uint32_t j) -> const uint8_t* {
         if constexpr (TBL)
-            return reinterpret_cast<const uint8_t*>(tp[j]);
+            return kj->ptr[j];
         else
             return kj->in[j];
     };
     auto out_ptr = [&](uint32_t i) -> uint8_t* {
         if constexpr (TBL)
-            return reinterpret_cast<uint8_t*>(tp[k + i]);
+            return const_cast<uint8_t*>(kj->ptr[k + i]);
         else
             return kj->out[i];
     };
     const uint64_t sz = job.sz;
     uint32_t s = blockIdx.x / job.cps, c = blockIdx.x - s * job.cps;
     while (s < ns * ng) {
-        const uint32_t g = TBL ? s / ns : 0u, stripe = TBL ? s - g * ns : s;
+        const uint32_t g = TBL && ng > 1 ? s / ns : 0u, stripe = s - g * ns;
         const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
         const uint32_t r0 = gr0 + wave * grn / nw, rows = gr0 + (wave + 1) * grn / nw - r0;
-        KWords cw;
+        CU64 ca;
         if constexpr (TBL)
-            cw = (KWords)(tp + k + r) + (g * nw + wave) * k * (RTP / 4);
+            ca = (CU64)job.addr + (g * nw + wave) * k * RT;
         else
-            cw = (KWords)kj->coef + wave * k * (RTP / 4);
+            ca = (CU64)kj->addr + wave * k * RT;
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;  // the last unit ends at sz (overlapping its neighbour)
         const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
         const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
-        uint32_t acc[RT][8];
-#pragma unroll
-        for (int rr = 0; rr < RT; ++rr)
-#pragma unroll
-            for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
+        uint32_t acc[RT][8];  // no zeroing: the wave's first input calls "set" routines (kBsrSetBase)
         for (uint32_t ph = 0; ph < k; ph += kp) {
             const uint32_t kn = k - ph < kp ? k - ph : kp;
             // inputs -> bit-planes -> LDS, inputs wave, wave + nw, ... in batches
@@ -1238,23 +1271,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
                 }
             }
             __syncthreads();
-            // input j's planes and coefficient words are read during input j - 1
-            // (one wait drains LDS and scalar loads alike)
-            uint32_t cwd[RTP / 4];
-#pragma unroll
-            for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[ph * (RTP / 4) + d];
-            for (uint32_t j = 0; j < kn; ++j) {
+            // the phase's inputs in pairs with fixed address registers (A: even,
+            // B: odd): after input j's calls its set is reloaded (scalar loads,
+            // unconditional: clamped to the phase's last input) with input j + 2's
+            // addresses, which have all of input j + 1 to arrive (one wait drains
+            // LDS and scalar loads alike)
+            uint64_t ada[RT], adb[RT];
+            bsr_addrs<RT>(ada, ca, ph);
+            bsr_addrs<RT>(adb, ca, ph + (kn > 1 ? 1 : 0));
+            auto step = [&](uint32_t j, uint64_t (&ad)[RT]) {
                 const u32x4 pa = bsr_planes[j * 128u + lane], pb = bsr_planes[j * 128u + 64u + lane];
                 const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-                uint32_t offs[RT];
-#pragma unroll
-                for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
-                if (j + 1 < kn) {
-#pragma unroll
-                    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[(ph + j + 1) * (RTP / 4) + d];
-                }
-                bsr_input<RT>(acc, p, offs);
+                bsr_input<RT>(acc, p, ad);
+                bsr_addrs<RT>(ad, ca, ph + (j + 2 < kn ? j + 2 : kn - 1));
+            };
+            uint32_t j = 0;
+            for (; j + 1 < kn; j += 2) {
+                step(j, ada);
+                step(j + 1, adb);
             }
+            if (j < kn) step(j, ada);
             __syncthreads();  // every wave has read the planes before they are overwritten
         }
 #pragma unroll
@@ -1276,15 +1312,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
 }
 
 // One wave's walk over n inputs of a unit (the one-wave and ks forms): input
-// j's two 16-byte pieces at ptr(j) + ib, its coefficient words at cw[j * RTP/4].
+// j's two 16-byte pieces at ptr(j) + ib, its routine addresses at ca[j * RT].
 // Unrolled by two with fixed register roles (A: even inputs, B: odd), so a
 // load lands in the registers its input's transpose has just consumed (no
-// copies) and is waited for two inputs later; block pointers and coefficient
-// words are scalar-loaded one step ahead of their use (a scalar wait drains
-// every outstanding scalar load, so none is issued right before it is needed).
+// copies) and is waited for two inputs later; the A and B routine-address
+// sets are scalar-loaded the same way, and block pointers one step ahead of
+// their use (a scalar wait drains every outstanding scalar load, so none is
+// issued right before it is needed).
 template <int RT, class P>
-__device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uint64_t ib, KWords cw, P ptr) {
-    constexpr uint32_t RTP = bsr_rtp<RT>();
+__device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uint64_t ib, CU64 ca, P ptr) {
     u32x4 a0, a1, b0, b1;
     const uint8_t* pa = ptr(0);
     const uint8_t* pb = ptr(n > 1 ? 1 : 0);
@@ -1294,24 +1330,19 @@ __device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uin
     b1 = load16(pb + ib + 1024);
     pa = ptr(n > 2 ? 2 : n - 1);
     pb = ptr(n > 3 ? 3 : n - 1);
-    uint32_t cwd[RTP / 4];
-#pragma unroll
-    for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[d];
+    uint64_t ada[RT], adb[RT];
+    bsr_addrs<RT>(ada, ca, 0);
+    bsr_addrs<RT>(adb, ca, n > 1 ? 1 : 0);
     // the loads and scalar loads are unconditional (past the last input they
     // re-read input n - 1, from L2): a conditional load would make the compiler
     // merge its registers with a copy that waits for every load in flight
-    auto step = [&](u32x4& x0, u32x4& x1, const uint8_t*& pn, uint32_t j) {
+    auto step = [&](u32x4& x0, u32x4& x1, const uint8_t*& pn, uint64_t (&ad)[RT], uint32_t j) {
         uint32_t p[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         transpose8(p);
-        uint32_t offs[RT];
-#pragma unroll
-        for (int rr = 0; rr < RT; ++rr) offs[rr] = ((cwd[rr / 4] >> ((rr % 4) * 8)) & 0xFFu) * kBsrStride;
-        const uint32_t jn = j + 1 < n ? j + 1 : j;
-#pragma unroll
-        for (uint32_t d = 0; d < RTP / 4; ++d) cwd[d] = cw[jn * (RTP / 4) + d];
-        bsr_input<RT>(acc, p, offs);
-        // input j + 2 into x0 / x1, which the transpose has consumed (after the
-        // calls, so the compiler cannot keep the planes in them and copy)
+        bsr_input<RT>(acc, p, ad);
+        // input j + 2 into x0 / x1 / ad, which this input has consumed (after
+        // the calls, so the compiler cannot keep the planes in them and copy)
+        bsr_addrs<RT>(ad, ca, j + 2 < n ? j + 2 : n - 1);
         x0 = load16(pn + ib);
         x1 = load16(pn + ib + 1024);
         pn = ptr(j + 4 < n ? j + 4 : n - 1);
@@ -1320,21 +1351,20 @@ __device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uin
     // loop, input j's wait leaves input j + 1's loads in flight
     uint32_t j = 0;
     for (; j + 1 < n; j += 2) {
-        step(a0, a1, pa, j);
-        step(b0, b1, pb, j + 1);
+        step(a0, a1, pa, ada, j);
+        step(b0, b1, pb, adb, j + 1);
     }
-    if (j < n) step(a0, a1, pa, j);
+    if (j < n) step(a0, a1, pa, ada, j);
 }
 
 // One wave per (unit, row tile), no LDS: the wave loads and transposes every
 // input of its unit itself (tiles of one unit are adjacent workgroups, so the
 // second tile's loads hit L2), two inputs in flight ahead.
 template <int RT>
-__global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
-    constexpr uint32_t RTP = bsr_rtp<RT>();
+__global__ __launch_bounds__(64) void matapply_bsr_solo(const BsrJob job) {
     const uint32_t lane = threadIdx.x;
-    const uint32_t k = job.k, r = job.r, nt = job.pad_;
-    const KPtr<MatJob> kj = kernarg_job<MatJob>();
+    const uint32_t k = job.k, r = job.r, nt = job.nt;
+    const KPtr<BsrJob> kj = kernarg_job<BsrJob>();
     const uint64_t sz = job.sz;
     const uint64_t total = uint64_t(job.nstripes) * job.cps * nt;
     for (uint64_t v = blockIdx.x; v < total; v += gridDim.x) {
@@ -1342,17 +1372,13 @@ __global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
         const uint64_t u = v / nt;
         const uint32_t s = static_cast<uint32_t>(u / job.cps), c = static_cast<uint32_t>(u % job.cps);
         const uint32_t r0 = t * r / nt, rows = (t + 1) * r / nt - r0;
-        const KWords cw = (KWords)kj->coef + t * k * (RTP / 4);
+        const CU64 ca = (CU64)kj->addr + t * k * RT;
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;
         const uint64_t ib = s * job.in_sstride + off + lane * 16u;
         const uint64_t ob = s * job.out_sstride + off + lane * 16u;
-        uint32_t acc[RT][8];
-#pragma unroll
-        for (int rr = 0; rr < RT; ++rr)
-#pragma unroll
-            for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
-        bsr_walk<RT>(acc, k, ib, cw, [&](uint32_t j) { return kj->in[j]; });
+        uint32_t acc[RT][8];  // no zeroing: the wave's first input calls "set" routines (kBsrSetBase)
+        bsr_walk<RT>(acc, k, ib, ca, [&](uint32_t j) { return kj->in[j]; });
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
             if (static_cast<uint32_t>(rr) < rows) {
@@ -1371,18 +1397,16 @@ __global__ __launch_bounds__(64) void matapply_bsr_solo(const MatJob job) {
 // [w k / W, (w + 1) k / W), loaded two ahead and transposed by the wave), XOR
 // their partial accumulator planes into one LDS copy of the unit's rows
 // (ds_xor_b32, [row][plane][lane]), and after a barrier wave w transposes and
-// stores rows w, w + W, ...  Block pointers and coefficients come from a
-// device-side table (BsrTblJob::table: k input pointers, r output pointers,
-// then [input][RTP] coefficient bytes).
+// stores rows w, w + W, ...  Block pointers in the arguments, routine
+// addresses ([group][input][RT]) in the device-side table (BsrTblJob).
 template <int RT>
 __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
-    constexpr uint32_t RTP = bsr_rtp<RT>();
     __shared__ uint32_t red[RT * 8 * 64];  // [row][plane][lane]
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
-    const CU64 tp = (CU64)job.table;
+    const KPtr<BsrTblJob> kj = kernarg_job<BsrTblJob>();
     const uint32_t j0 = wave * k / nw, j1 = (wave + 1) * k / nw;
     const uint32_t ns = job.nstripes, ng = job.ngroups;  // row groups of <= RT rows: (group, stripe) walk
     const uint64_t sz = job.sz;
@@ -1392,19 +1416,15 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
     while (s < ns * ng) {
         const uint32_t g = s / ns, stripe = s - g * ns;
         const uint32_t gr0 = g * r / ng, rows = (g + 1) * r / ng - gr0;
-        const KWords cw = (KWords)(tp + k + r) + g * k * (RTP / 4);
+        const CU64 ca = (CU64)job.addr + g * k * RT;
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;
         const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
         const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
         if (j0 < j1) {  // wave-uniform
-            uint32_t acc[RT][8];
-#pragma unroll
-            for (int rr = 0; rr < RT; ++rr)
-#pragma unroll
-                for (int b = 0; b < 8; ++b) acc[rr][b] = 0u;
-            bsr_walk<RT>(acc, j1 - j0, ib, cw + j0 * (RTP / 4),
-                         [&](uint32_t j) { return reinterpret_cast<const uint8_t*>(tp[j0 + j]); });
+            uint32_t acc[RT][8];  // no zeroing: input j0 calls "set" routines (kBsrSetBase)
+            bsr_walk<RT>(acc, j1 - j0, ib, ca + j0 * RT,
+                         [&](uint32_t j) { return kj->ptr[j0 + j]; });
 #pragma unroll
             for (int rr = 0; rr < RT; ++rr)
                 if (static_cast<uint32_t>(rr) < rows)
@@ -1422,7 +1442,7 @@ __global__ __launch_bounds__(512) void matapply_bsr_ks(const BsrTblJob job) {
                 red[(i * 8 + b) * 64 + lane] = 0u;  // ready for the next unit
             }
             transpose8(v);
-            uint8_t* op = reinterpret_cast<uint8_t*>(tp[k + gr0 + i]) + ob;
+            uint8_t* op = const_cast<uint8_t*>(kj->ptr[k + gr0 + i]) + ob;
             store16_out<true>(op, u32x4{v[0], v[1], v[2], v[3]});
             store16_out<true>(op + 1024, u32x4{v[4], v[5], v[6], v[7]});
         }
@@ -2014,11 +2034,186 @@ std::once_flag g_bsr_once;
 
 template <int RT>
 void fill_bsr() {
-    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, false, MatJob>);
+    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, false, BsrJob>);
     snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d,lds>", RT);
     g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
     snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d>", RT);
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
+}
+
+// The address of the routine table on each device, read once per device by
+// bsr_table_probe (the host writes every coefficient's routine address into the
+// launches' arguments).  A device whose probe fails gets no matapply_bsr
+// launches: launch_apply hands them to matapply_bsg.
+constexpr int kBsrMaxDevices = 64;
+struct BsrBase {
+    std::once_flag once;
+    uint64_t addr = 0;
+};
+BsrBase g_bsr_base[kBsrMaxDevices];
+
+hipError_t bsr_routine_base(uint64_t* base) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kBsrMaxDevices) return hipErrorNotSupported;
+    BsrBase& b = g_bsr_base[dev];
+    std::call_once(b.once, [&b] {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
+        uint64_t* h = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(uint64_t), hipHostMallocDefault) == hipSuccess) {
+            *h = 0;
+            hipLaunchKernelGGL(bsr_table_probe, dim3(1), dim3(64), 0, st, h);
+            if (hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess) b.addr = *h;
+            (void)hipHostFree(h);
+        }
+        (void)hipStreamDestroy(st);
+    });
+    if (!b.addr) return hipErrorNotSupported;
+    *base = b.addr;
+    return hipSuccess;
+}
+
+// Routine addresses in a bsr kernel's walk order, [group][wave][input][rt]:
+// group g holds rows g*r/ng .. (g+1)*r/ng - 1, split over its nw waves as the
+// kernels split them; routine 0 (which only returns) past a wave's rows.  The
+// first input a wave walks -- input 0, or with the inputs split over `split`
+// waves (the ks form) inputs s*k/split -- calls the "set" routines, which
+// write the rows instead of adding to them (the kernels do not zero their
+// accumulators).  False if a wave would hold more than rt rows (the kernel
+// would drop them).
+bool fill_bsr_addrs(uint64_t* dst, const ApplySpec& a, uint64_t base, uint32_t ng, uint32_t nw, uint32_t rt,
+                    uint32_t split) {
+    const uint32_t k = a.k, r = a.r;
+    std::vector<uint8_t> first(k, 0);
+    for (uint32_t w = 0; w < split; ++w)
+        if (w * k / split < (w + 1) * k / split) first[w * k / split] = 1;
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t r0 = gr0 + w * grn / nw, rows = gr0 + (w + 1) * grn / nw - r0;
+            if (rows > rt) return false;
+            uint64_t* d = dst + size_t(g * nw + w) * k * rt;
+            for (uint32_t j = 0; j < k; ++j) {
+                const uint64_t tb = base + (first[j] ? kBsrSetBase : 0u);
+                for (uint32_t rr = 0; rr < rt; ++rr)
+                    d[size_t(j) * rt + rr] =
+                        tb + uint64_t(kBsrStride) * (rr < rows ? a.coef[size_t(r0 + rr) * a.coef_stride + j] : 0u);
+            }
+        }
+    }
+    return true;
+}
+
+// Device-side routine-address tables of the table forms, kept per (thread,
+// device) by matrix and layout: a launch whose table is held reads it as is
+// (its block pointers travel in the kernel arguments), so a matrix's table is
+// copied to the device by its first launch only.  Copying the table per launch
+// cost 19 us ahead of each 0.10 ms 200/256 launch (90 KB of addresses).  Slots
+// are reused round-robin once the launches that read them have finished (an
+// event per slot); a launch on another stream than the slot's last one is
+// ordered after it (hipStreamWaitEvent), so one event covers every reader.
+struct BsrTblCache {
+    static constexpr int kSlots = 8;
+    static constexpr size_t kSlotBytes = size_t(160) << 10;
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    hipEvent_t used[kSlots] = {};  // recorded after the last launch that read the slot (and its upload)
+    bool busy[kSlots] = {};
+    hipStream_t last[kSlots] = {};
+    uint32_t dims[kSlots][6] = {};  // k, r, ng, nw, rt, split of the table held (k == 0: empty)
+    std::vector<uint8_t> coef[kSlots];
+    unsigned next = 0;
+};
+
+struct BsrTblCaches {
+    std::unordered_map<int, BsrTblCache> dev;
+    ~BsrTblCaches() {
+        for (auto& kv : dev) {
+            int cur = 0;
+            if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(kv.first) != hipSuccess) continue;
+            BsrTblCache& c = kv.second;
+            for (int i = 0; i < BsrTblCache::kSlots; ++i)
+                if (c.used[i]) (void)hipEventSynchronize(c.used[i]), (void)hipEventDestroy(c.used[i]);
+            if (c.dev) (void)hipFree(c.dev);
+            if (c.host) (void)hipHostFree(c.host);
+            (void)hipSetDevice(cur);
+        }
+    }
+};
+thread_local BsrTblCaches t_bsr_tbl;
+
+struct BsrTblRef {
+    BsrTblCache* c = nullptr;
+    unsigned slot = 0;
+    const uint64_t* dev = nullptr;
+};
+
+hipError_t bsr_table_done(const BsrTblRef& t, hipStream_t stream) {
+    const hipError_t e = hipEventRecord(t.c->used[t.slot], stream);
+    if (e == hipSuccess) {
+        t.c->busy[t.slot] = true;
+        t.c->last[t.slot] = stream;
+    }
+    return e;
+}
+
+// The device-side address table of a (matrix, layout) for a launch on `stream`
+// (ng row groups of nw waves of rt rows, inputs split over `split` waves),
+// uploaded on a miss; the caller
+// launches, then calls bsr_table_done.
+hipError_t bsr_addr_table(const ApplySpec& a, hipStream_t stream, uint64_t base, uint32_t ng, uint32_t nw, uint32_t rt,
+                          uint32_t split, BsrTblRef* ref) {
+    const uint32_t k = a.k, r = a.r;
+    const size_t n = size_t(ng) * nw * k * rt;
+    if (n * 8 > BsrTblCache::kSlotBytes) return hipErrorNotSupported;
+    int devid = 0;
+    hipError_t e = hipGetDevice(&devid);
+    if (e != hipSuccess) return e;
+    BsrTblCache& c = t_bsr_tbl.dev[devid];
+    if (!c.dev) {
+        if ((e = hipMalloc(&c.dev, BsrTblCache::kSlots * BsrTblCache::kSlotBytes)) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&c.host, BsrTblCache::kSlots * BsrTblCache::kSlotBytes, hipHostMallocDefault)) !=
+            hipSuccess) {
+            (void)hipFree(c.dev);
+            c.dev = nullptr;
+            return e;
+        }
+        for (int i = 0; i < BsrTblCache::kSlots; ++i)
+            if ((e = hipEventCreateWithFlags(&c.used[i], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    thread_local std::vector<uint8_t> m;  // the matrix, row-major: the key with the layout
+    m.resize(size_t(r) * k);
+    for (uint32_t i = 0; i < r; ++i) std::memcpy(&m[size_t(i) * k], a.coef + size_t(i) * a.coef_stride, k);
+    const uint32_t dims[6] = {k, r, ng, nw, rt, split};
+    for (unsigned i = 0; i < BsrTblCache::kSlots; ++i) {
+        if (std::memcmp(c.dims[i], dims, sizeof dims) != 0 || c.coef[i] != m) continue;
+        if (c.busy[i] && c.last[i] != stream && (e = hipStreamWaitEvent(stream, c.used[i], 0)) != hipSuccess)
+            return e;
+        *ref = BsrTblRef{&c, i, reinterpret_cast<const uint64_t*>(c.dev + i * BsrTblCache::kSlotBytes)};
+        return hipSuccess;
+    }
+    const unsigned i = c.next++ % BsrTblCache::kSlots;
+    if (c.busy[i] && (e = hipEventSynchronize(c.used[i])) != hipSuccess) return e;  // its readers have finished
+    c.busy[i] = false;
+    c.dims[i][0] = 0;  // empty until the upload is enqueued
+    uint64_t* h = reinterpret_cast<uint64_t*>(c.host + i * BsrTblCache::kSlotBytes);
+    uint8_t* d = c.dev + i * BsrTblCache::kSlotBytes;
+    if (!fill_bsr_addrs(h, a, base, ng, nw, rt, split)) return hipErrorInvalidValue;
+    if ((e = hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    if ((e = bsr_table_done(BsrTblRef{&c, i, nullptr}, stream)) != hipSuccess) return e;  // the upload is a reader too
+    std::memcpy(c.dims[i], dims, sizeof dims);
+    c.coef[i] = m;
+    *ref = BsrTblRef{&c, i, reinterpret_cast<const uint64_t*>(d)};
+    return hipSuccess;
+}
+
+// Block pointers of a table-form launch into its arguments: false if k + r
+// exceeds them.
+bool bsr_tbl_ptrs(const ApplySpec& a, BsrTblJob& job) {
+    if (size_t(a.k) + a.r > static_cast<size_t>(kBsrTblPtrs)) return false;
+    for (uint32_t j = 0; j < a.k; ++j) job.ptr[j] = a.in[j];
+    for (uint32_t i = 0; i < a.r; ++i) job.ptr[a.k + i] = a.out[i];
+    return true;
 }
 
 // Waves (row tiles) per workgroup: one for r <= 10 (the one-wave form); 4 for
@@ -2040,13 +2235,9 @@ void bsr_tiles(uint32_t r, uint64_t units, uint32_t* nw, uint32_t* rt) {
 }
 
 bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
-    if (generic_mode() != 2 || k < 1 || k > static_cast<uint32_t>(kMaxIn) || r < 1 ||
-        r > 4u * kBsrMaxRows || sz < kBsrChunk || k * r < 24 || (k <= 4 && r <= 8))
-        return false;
-    // the largest coefficient block any launch of this shape lays out (4 tiles)
-    const uint32_t rt4 = (r + 3) / 4;
-    return r <= 4u * kBsrMaxRows && 4 * k * ((rt4 + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef) &&
-           2 * k * (((r + 1) / 2 + 3) / 4 * 4) <= static_cast<uint32_t>(kMaxCoef);
+    // kernel-argument form, or the table form past kBsrArgAddrs addresses
+    return generic_mode() == 2 && k >= 1 && k <= static_cast<uint32_t>(kMaxIn) && r >= 1 &&
+           r <= static_cast<uint32_t>(kBsrMaxOut) && sz >= kBsrChunk && k * r >= 24 && !(k <= 4 && r <= 8);
 }
 
 // Wide codes, one row tile: matapply_bsr_ks (table form).  Waves per unit:
@@ -2093,9 +2284,11 @@ void fill_bsr_ks() {
 
 hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_ks_once, [] { fill_bsr_ks<1>(); });
+    uint64_t base = 0;
+    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
     const uint32_t k = a.k, r = a.r;
     const uint32_t ng = r <= static_cast<uint32_t>(kBsrMaxRows) ? 1u : (r + kBsrKsRows - 1) / kBsrKsRows;
-    const uint32_t rt = (r + ng - 1) / ng, rtp = (rt + 3) / 4 * 4;
+    const uint32_t rt = (r + ng - 1) / ng;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
     const uint64_t units = cps * a.nstripes * ng;
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
@@ -2104,26 +2297,11 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     // 0.031 ms per 64 MiB stripe) and the same on 255/256
     uint32_t nw = units * 2 < uint64_t(g_num_cu) * 4 ? 8u : 4u;
     while (nw > 1 && k / nw < 4) nw /= 2;
-    const size_t bytes = 8 * size_t(k + r) + size_t(ng) * k * rtp;
-    if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
-    TableRing* ring = nullptr;
-    unsigned slot = 0;
-    hipError_t e = ring_slot(&ring, &slot);
-    if (e != hipSuccess) return e;
-    uint8_t* h = ring->host + slot * TableRing::kSlotBytes;
-    uint8_t* d = ring->dev + slot * TableRing::kSlotBytes;
-    std::memcpy(h, a.in, 8 * size_t(k));
-    std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
-    uint8_t* cf = h + 8 * size_t(k + r);
-    std::memset(cf, 0, size_t(ng) * k * rtp);
-    for (uint32_t g = 0; g < ng; ++g) {
-        const uint32_t gr0 = g * r / ng, rows = (g + 1) * r / ng - gr0;
-        for (uint32_t j = 0; j < k; ++j)
-            for (uint32_t i = 0; i < rows; ++i)
-                cf[(size_t(g) * k + j) * rtp + i] = a.coef[size_t(gr0 + i) * a.coef_stride + j];
-    }
-    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
     BsrTblJob job;
+    if (!bsr_tbl_ptrs(a, job)) return hipErrorNotSupported;
+    BsrTblRef t;
+    hipError_t e = bsr_addr_table(a, stream, base, ng, 1, rt, nw, &t);
+    if (e != hipSuccess) return e;
     job.sz = a.sz;
     job.in_sstride = a.in_sstride;
     job.out_sstride = a.out_sstride;
@@ -2137,12 +2315,10 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
-    job.table = d;
+    job.addr = t.dev;
     if ((e = launch_job(g_bsr_ks[rt].fn, grid, 64 * nw, 0, stream, job)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
-    ring->busy[slot] = true;
     t_last_kernel = g_bsr_ks[rt].name;
-    return hipSuccess;
+    return bsr_table_done(t, stream);
 }
 
 // Table form of the LDS-phase kernel: k > 32 with more than one row tile, or
@@ -2159,52 +2335,31 @@ struct BsrTblVariant {
     const void* fn = nullptr;
     char name[28] = "";
 };
-BsrTblVariant g_bsr_tbl[kBsrTblTile + 1];
+BsrTblVariant g_bsr_tbl[kBsrMaxRows + 1];
 std::once_flag g_bsr_tbl_once;
 
 template <int RT>
 void fill_bsr_tbl() {
     g_bsr_tbl[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, true, BsrTblJob>);
     snprintf(g_bsr_tbl[RT].name, sizeof g_bsr_tbl[RT].name, "matapply_bsr<%d,lds,tbl>", RT);
-    if constexpr (RT < static_cast<int>(kBsrTblTile)) fill_bsr_tbl<RT + 1>();
+    if constexpr (RT < kBsrMaxRows) fill_bsr_tbl<RT + 1>();
 }
 
-hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
+// One table-form launch of the LDS-phase kernel: ng row groups of nw waves of
+// <= rt rows each.
+hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t base, uint32_t ng, uint32_t nw,
+                              uint32_t rt) {
     std::call_once(g_bsr_tbl_once, [] { fill_bsr_tbl<1>(); });
     const uint32_t k = a.k, r = a.r;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
-    const uint32_t tile = bsr_tbl_tile(k, r, cps * a.nstripes);
-    const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
-    const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
-    uint32_t nw = 1;                                   // 1, 2, 4 or 8 waves: see bsr_tiles
-    while (nw * tile < rpg) nw *= 2;
-    const uint32_t rt = (rpg + nw - 1) / nw, rtp = (rt + 3) / 4 * 4;
     const uint64_t vunits = cps * a.nstripes * ng;
-    if (vunits >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
-    const size_t cbytes = size_t(ng) * nw * k * rtp;
-    const size_t bytes = 8 * size_t(k + r) + cbytes;
-    if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
-    TableRing* ring = nullptr;
-    unsigned slot = 0;
-    hipError_t e = ring_slot(&ring, &slot);
-    if (e != hipSuccess) return e;
-    uint8_t* h = ring->host + slot * TableRing::kSlotBytes;
-    uint8_t* d = ring->dev + slot * TableRing::kSlotBytes;
-    std::memcpy(h, a.in, 8 * size_t(k));
-    std::memcpy(h + 8 * size_t(k), a.out, 8 * size_t(r));
-    uint8_t* cf = h + 8 * size_t(k + r);
-    std::memset(cf, 0, cbytes);
-    for (uint32_t g = 0; g < ng; ++g) {
-        const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
-        for (uint32_t w = 0; w < nw; ++w) {
-            const uint32_t r0 = gr0 + w * grn / nw, rows = gr0 + (w + 1) * grn / nw - r0;
-            for (uint32_t j = 0; j < k; ++j)
-                for (uint32_t rr = 0; rr < rows; ++rr)
-                    cf[((size_t(g) * nw + w) * k + j) * rtp + rr] = a.coef[size_t(r0 + rr) * a.coef_stride + j];
-        }
-    }
-    if ((e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    if (vunits >= (1ull << 32) - (1ull << 24) || rt < 1 || rt > static_cast<uint32_t>(kBsrMaxRows))
+        return hipErrorInvalidValue;
     BsrTblJob job;
+    if (!bsr_tbl_ptrs(a, job)) return hipErrorNotSupported;
+    BsrTblRef t;
+    hipError_t e = bsr_addr_table(a, stream, base, ng, nw, rt, 1, &t);
+    if (e != hipSuccess) return e;
     job.sz = a.sz;
     job.in_sstride = a.in_sstride;
     job.out_sstride = a.out_sstride;
@@ -2218,45 +2373,60 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
-    job.table = d;
+    job.addr = t.dev;
     const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
     if ((e = launch_job(g_bsr_tbl[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job)) != hipSuccess)
         return e;
-    if ((e = hipEventRecord(ring->ev[slot], stream)) != hipSuccess) return e;
-    ring->busy[slot] = true;
     t_last_kernel = g_bsr_tbl[rt].name;
-    return hipSuccess;
+    return bsr_table_done(t, stream);
+}
+
+hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
+    uint64_t base = 0;
+    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
+    const uint32_t r = a.r;
+    const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
+    const uint32_t tile = bsr_tbl_tile(a.k, r, cps * a.nstripes);
+    const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
+    const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
+    uint32_t nw = 1;                                   // 1, 2, 4 or 8 waves: see bsr_tiles
+    while (nw * tile < rpg) nw *= 2;
+    return launch_bsr_lds_tbl(a, stream, base, ng, nw, (rpg + nw - 1) / nw);
 }
 
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_once, [] { fill_bsr<1>(); });
+    uint64_t base = 0;
+    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
     const uint32_t k = a.k, r = a.r;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
     const uint64_t units = cps * a.nstripes;
     uint32_t nw, rt;
     bsr_tiles(r, units, &nw, &rt);
-    const uint32_t rtp = (rt + 3) / 4 * 4;
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
-    MatJob job;
-    fill_matjob(a, job);
-    std::memset(job.coef, 0, size_t(nw) * k * rtp);
-    for (uint32_t w = 0; w < nw; ++w) {
-        const uint32_t r0 = w * r / nw, rows = (w + 1) * r / nw - r0;
-        for (uint32_t j = 0; j < k; ++j)
-            for (uint32_t rr = 0; rr < rows; ++rr)
-                job.coef[(w * k + j) * rtp + rr] = a.coef[size_t(r0 + rr) * a.coef_stride + j];
-    }
+    // more addresses than the arguments hold (e.g. K=20/M=60's 40-row encode):
+    // the same kernel reading them from a device-side table
+    if (size_t(nw) * k * rt > static_cast<size_t>(kBsrArgAddrs)) return launch_bsr_lds_tbl(a, stream, base, 1, nw, rt);
+    BsrJob job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = k;
+    job.r = r;
+    job.nt = nw;
+    job.pad_ = 0;
+    for (uint32_t j = 0; j < k; ++j) job.in[j] = a.in[j];
+    for (uint32_t i = 0; i < r; ++i) job.out[i] = a.out[i];
+    if (!fill_bsr_addrs(job.addr, a, base, 1, nw, rt, 1)) return hipErrorInvalidValue;
     const uint64_t cap = uint64_t(g_num_cu) * 1024;
     const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
     job.cps = static_cast<uint32_t>(cps);
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
     if (nw == 1) {  // one row tile: one wave per unit, no LDS
-        job.pad_ = 1;
-        const uint64_t capw = uint64_t(g_num_cu) * 1024;
         t_last_kernel = g_bsr_var[rt].name_solo;
-        return launch_job(g_bsr_var[rt].fn_solo, static_cast<uint32_t>(units < capw ? units : capw), 64, 0, stream,
-                          job);
+        return launch_job(g_bsr_var[rt].fn_solo, grid, 64, 0, stream, job);
     }
     const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
     t_last_kernel = g_bsr_var[rt].name;
@@ -2326,8 +2496,14 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
     const bool reg = k <= static_cast<uint32_t>(kRegK) && r <= static_cast<uint32_t>(kRegR);
     if (wide) {
         if (a.accumulate || !bsg_shape_ok(k, r, a.sz)) return hipErrorNotSupported;
-        if (bsr_wide_ok(k, r, a.sz, a.nstripes)) return launch_bsr_wide(a, stream);
-        if (bsr_tbl_ok(k, r, a.sz)) return launch_bsr_tbl(a, stream);
+        // matapply_bsr, or matapply_bsg where it declines (hipErrorNotSupported:
+        // a table past its ring slot, or no routine table on this device)
+        hipError_t e = hipErrorNotSupported;
+        if (bsr_wide_ok(k, r, a.sz, a.nstripes))
+            e = launch_bsr_wide(a, stream);
+        else if (bsr_tbl_ok(k, r, a.sz))
+            e = launch_bsr_tbl(a, stream);
+        if (e != hipErrorNotSupported) return e;
         return launch_bsg(a, stream);
     }
     const Config& cfg = config();
@@ -2341,8 +2517,14 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
             return se;
         }
     }
-    if (!a.accumulate && bsr_shape_ok(k, r, a.sz)) return launch_bsr(a, stream);
-    if (!a.accumulate && bsr_tbl_ok(k, r, a.sz)) return launch_bsr_tbl(a, stream);
+    if (!a.accumulate) {
+        hipError_t e = hipErrorNotSupported;
+        if (bsr_shape_ok(k, r, a.sz))
+            e = launch_bsr(a, stream);
+        else if (bsr_tbl_ok(k, r, a.sz))
+            e = launch_bsr_tbl(a, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
     if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);
