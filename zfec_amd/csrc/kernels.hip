@@ -1878,6 +1878,12 @@ bool bsg_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
 // device: a ring of slots in device memory filled by stream-ordered copies
 // from a pinned mirror; a slot is reused once the event recorded after its
 // last launch has completed.
+// Events that only tell the host when a table slot's readers have finished
+// (hipEventSynchronize before the slot is rewritten, hipStreamWaitEvent for
+// another stream of the same device): no system-scope release, which would
+// write the L2's dirty lines back at every launch that records one.
+constexpr unsigned kSlotEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
 struct TableRing {
     static constexpr int kSlots = 8;
     static constexpr size_t kSlotBytes = size_t(160) << 10;  // k, r <= 256 with 64 row groups of 4
@@ -1919,7 +1925,7 @@ hipError_t ring_slot(TableRing** ring, unsigned* slot) {
             return e;
         }
         for (int i = 0; i < TableRing::kSlots; ++i)
-            if ((e = hipEventCreateWithFlags(&t.ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+            if ((e = hipEventCreateWithFlags(&t.ev[i], kSlotEventFlags)) != hipSuccess) return e;
     }
     const unsigned s = t.next++ % TableRing::kSlots;
     if (t.busy[s] && (e = hipEventSynchronize(t.ev[s])) != hipSuccess) return e;  // its last launch has read it
@@ -2179,7 +2185,7 @@ hipError_t bsr_addr_table(const ApplySpec& a, hipStream_t stream, uint64_t base,
             return e;
         }
         for (int i = 0; i < BsrTblCache::kSlots; ++i)
-            if ((e = hipEventCreateWithFlags(&c.used[i], hipEventDisableTiming)) != hipSuccess) return e;
+            if ((e = hipEventCreateWithFlags(&c.used[i], kSlotEventFlags)) != hipSuccess) return e;
     }
     thread_local std::vector<uint8_t> m;  // the matrix, row-major: the key with the layout
     m.resize(size_t(r) * k);
