@@ -326,8 +326,8 @@ def _bsr_traced_name(printed):
     a = printed[len("matapply_bsr<"):-1].split(",")
     rt = a[0]
     form = ",".join(a[1:])
-    return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, zfec_hip::MatJob>" % rt,
-            "lds,tbl": "matapply_bsr<%s, true, zfec_hip::BsrTblJob>" % rt,
+    return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, BsrJob>" % rt,
+            "lds,tbl": "matapply_bsr<%s, true, BsrTblJob>" % rt,
             "ks,tbl": "matapply_bsr_ks<%s>" % rt}.get(form)
 
 

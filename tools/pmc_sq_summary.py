@@ -36,7 +36,7 @@ def summarize(tag, workloads):
                 for r in csv.DictReader(f):
                     if "zfec" not in r["Kernel_Name"]:
                         continue
-                    n = r["Kernel_Name"].replace("void zfec_hip::(anonymous namespace)::", "").split("(")[0]
+                    n = r["Kernel_Name"].replace("zfec_hip::(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0]
                     agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
             for n, v in agg.items():
                 ws.setdefault(n, {}).update({c: round(sum(x) / len(x)) for c, x in v.items()})

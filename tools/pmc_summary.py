@@ -30,8 +30,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    name = name.replace("void zfec_hip::(anonymous namespace)::", "")
-    return name.split("(zfec_hip::MatJob)")[0].split("(Args)")[0][:80]
+    name = name.replace("zfec_hip::(anonymous namespace)::", "").replace("void ", "", 1)
+    return name.split("(")[0][:80]
 
 
 def load(path):

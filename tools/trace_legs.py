@@ -24,7 +24,7 @@ import sys
 def short(name):
     """'void zfec_hip::(anonymous namespace)::matapply_reg<3, 7, true, ...>(zfec_hip::MatJob)' ->
     ('matapply_reg', [3, 7]); 'zfec_hip_bitslice_k20_r40_<hash>' -> (itself, [])."""
-    n = name.replace("void zfec_hip::(anonymous namespace)::", "").split("(")[0]
+    n = name.replace("zfec_hip::(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0]
     if "<" not in n:
         return n, []
     base, args = n.split("<", 1)
