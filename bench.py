@@ -319,15 +319,18 @@ def device_tree_hash():
 
 def _bsr_traced_name(printed):
     """The library's matapply_bsr names -> the kernels' demangled names:
-    <RT> one-wave form, <RT,lds> LDS-phase form, <RT,lds,tbl> its table form,
+    <RT> one-wave form, <RT,lds> LDS-phase form, <RT,lds,tbl> its table form
+    (",cmb": the combination-sharing variant of either),
     <RT,ks,tbl> the input-split form (kernels.hip fill_bsr*)."""
     if not printed.startswith("matapply_bsr<"):
         return None
     a = printed[len("matapply_bsr<"):-1].split(",")
     rt = a[0]
     form = ",".join(a[1:])
-    return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, BsrJob>" % rt,
-            "lds,tbl": "matapply_bsr<%s, true, BsrTblJob>" % rt,
+    return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, false, BsrJob>" % rt,
+            "lds,cmb": "matapply_bsr<%s, false, true, BsrJob>" % rt,
+            "lds,tbl": "matapply_bsr<%s, true, false, BsrTblJob>" % rt,
+            "lds,tbl,cmb": "matapply_bsr<%s, true, true, BsrTblJob>" % rt,
             "ks,tbl": "matapply_bsr_ks<%s>" % rt}.get(form)
 
 

@@ -308,7 +308,8 @@ def tbl_name(r, units, k):
     nw = 1
     while nw * tile < rpg:
         nw *= 2
-    return "matapply_bsr<%d,lds,tbl>" % (-(-rpg // nw))
+    # 8-wave workgroups share the inputs' combinations through LDS (kernels.hip bsr_cmb)
+    return "matapply_bsr<%d,lds,tbl%s>" % (-(-rpg // nw), ",cmb" if nw >= 8 else "")
 
 
 # table form of the LDS-phase kernel: k > 32 with more than one row tile (row

@@ -61,6 +61,7 @@ namespace zfec_hip {
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -1138,6 +1139,9 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
 constexpr int kBsrBatch = 4;          // inputs a wave loads at once
 constexpr uint32_t kBsrPhase = 8;     // inputs whose planes share LDS at a time (multi-wave form)
+// Inputs per phase of the combination-sharing form (7.5 KiB each): one per wave,
+// so the 16 / nw workgroups a CU holds at 4 waves per SIMD take 120 KiB.
+__host__ __device__ constexpr uint32_t bsr_cmb_phase(uint32_t nw) { return nw; }
 constexpr int kBsrMaxOut = 4 * kBsrMaxRows;  // rows of the kernel-argument form (4 tiles)
 constexpr int kBsrArgAddrs = 432;     // routine addresses the kernel-argument form holds
 
@@ -1200,14 +1204,44 @@ __global__ void bsr_table_probe(uint64_t* out) {
     if (threadIdx.x == 0) out[0] = (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-template <int RT, bool TBL, class J>
+// The 30 combinations of an input's bit-planes in bsr_input_c's register
+// order (gf_routines.inc): planes p0..p7, then L[m] (planes 0-3) and H[m]
+// (planes 4-7) for the eleven multi-plane m in increasing order.
+__device__ __forceinline__ void bsr_combos(const uint32_t (&p)[8], uint32_t (&q)[30]) {
+    constexpr int kMulti[11] = {3, 5, 6, 7, 9, 10, 11, 12, 13, 14, 15};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = p[i];
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        uint32_t c[16] = {};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[1 << i] = p[4 * side + i];
+#pragma unroll
+        for (int x = 0; x < 11; ++x) {
+            const int m = kMulti[x];
+            const int top = m >= 8 ? 8 : m >= 4 ? 4 : 2;
+            c[m] = c[m ^ top] ^ c[top];
+            q[8 + 11 * side + x] = c[m];
+        }
+    }
+}
+
+// Bytes of LDS per input of a phase: the 8 planes, or (CMB) all 30 combinations.
+template <bool CMB>
+__host__ __device__ constexpr uint32_t bsr_in_bytes() {
+    return CMB ? 30u * 256u : 8u * 256u;
+}
+
+template <int RT, bool TBL, bool CMB, class J>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void matapply_bsr(const J job) {
-    extern __shared__ u32x4 bsr_planes[];  // [input][half][lane]
+    // [input][half][lane] planes, or (CMB) [input][7 x (4 dwords)][lane] + [2 dwords][lane] combinations
+    extern __shared__ u32x4 bsr_planes[];
+    constexpr uint32_t kIn = bsr_in_bytes<CMB>() / 16;  // u32x4 per input
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
-    constexpr uint32_t kp = kBsrPhase;
+    const uint32_t kp = CMB ? bsr_cmb_phase(nw) : kBsrPhase;
     constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
     // block pointers and routine addresses: kernel arguments (BsrJob) or the
     // device-side table (BsrTblJob); the walk's "stripes" are (row group,
@@ -1265,8 +1299,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
                         uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
                                          x[q][1].x, x[q][1].y, x[q][1].z, x[q][1].w};
                         transpose8(v);
-                        bsr_planes[j * 128u + lane] = u32x4{v[0], v[1], v[2], v[3]};
-                        bsr_planes[j * 128u + 64u + lane] = u32x4{v[4], v[5], v[6], v[7]};
+                        u32x4* b = bsr_planes + j * kIn;
+                        if constexpr (CMB) {  // every wave of the workgroup reads them: built once here
+                            uint32_t q[30];
+                            bsr_combos(v, q);
+#pragma unroll
+                            for (int g = 0; g < 7; ++g) b[g * 64 + lane] = u32x4{q[4 * g], q[4 * g + 1], q[4 * g + 2], q[4 * g + 3]};
+                            reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q[28], q[29]};
+                        } else {
+                            b[lane] = u32x4{v[0], v[1], v[2], v[3]};
+                            b[64u + lane] = u32x4{v[4], v[5], v[6], v[7]};
+                        }
                     }
                 }
             }
@@ -1280,9 +1323,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             bsr_addrs<RT>(ada, ca, ph);
             bsr_addrs<RT>(adb, ca, ph + (kn > 1 ? 1 : 0));
             auto step = [&](uint32_t j, uint64_t (&ad)[RT]) {
-                const u32x4 pa = bsr_planes[j * 128u + lane], pb = bsr_planes[j * 128u + 64u + lane];
-                const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-                bsr_input<RT>(acc, p, ad);
+                const u32x4* b = bsr_planes + j * kIn;
+                if constexpr (CMB) {
+                    uint32_t q[30];
+#pragma unroll
+                    for (int g = 0; g < 7; ++g) {
+                        const u32x4 t = b[g * 64 + lane];
+                        q[4 * g] = t.x;
+                        q[4 * g + 1] = t.y;
+                        q[4 * g + 2] = t.z;
+                        q[4 * g + 3] = t.w;
+                    }
+                    const u32x2 t2 = reinterpret_cast<const u32x2*>(b + 448)[lane];
+                    q[28] = t2.x;
+                    q[29] = t2.y;
+                    bsr_input_c<RT>(acc, q, ad);
+                } else {
+                    const u32x4 pa = b[lane], pb = b[64u + lane];
+                    const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+                    bsr_input<RT>(acc, p, ad);
+                }
                 bsr_addrs<RT>(ad, ca, ph + (j + 2 < kn ? j + 2 : kn - 1));
             };
             uint32_t j = 0;
@@ -2028,11 +2088,21 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 }
 
 // ---- matapply_bsr dispatch ------------------------------------------------------
+// Whether an nw-wave LDS-phase launch shares the inputs' 30 combinations through
+// LDS (built once per workgroup, phases of one input per wave) instead of the 8
+// planes (the 22 multi-plane combinations rebuilt by every wave): with 8 waves,
+// where rebuilding is 8x the work (128/256 0.130 -> 0.122 ms per 64 MiB stripe);
+// with 2 or 4 the short phases cost more than the XORs saved (cfg4's first-seen
+// 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json).
+bool bsr_cmb(uint32_t nw) { return nw >= 8; }
+
 // nw = ceil(r / 10) waves, one per row tile of <= RT = ceil(r / nw) rows.
 struct BsrVariant {
     const void* fn = nullptr;
+    const void* fn_cmb = nullptr;  // combination-sharing form (bsr_cmb)
     const void* fn_solo = nullptr;
     char name[24] = "";
+    char name_cmb[28] = "";
     char name_solo[32] = "";
 };
 BsrVariant g_bsr_var[kBsrMaxRows + 1];
@@ -2040,8 +2110,10 @@ std::once_flag g_bsr_once;
 
 template <int RT>
 void fill_bsr() {
-    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, false, BsrJob>);
+    g_bsr_var[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, false, false, BsrJob>);
+    g_bsr_var[RT].fn_cmb = reinterpret_cast<const void*>(matapply_bsr<RT, false, true, BsrJob>);
     snprintf(g_bsr_var[RT].name, sizeof g_bsr_var[RT].name, "matapply_bsr<%d,lds>", RT);
+    snprintf(g_bsr_var[RT].name_cmb, sizeof g_bsr_var[RT].name_cmb, "matapply_bsr<%d,lds,cmb>", RT);
     g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
     snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d>", RT);
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
@@ -2339,15 +2411,19 @@ bool bsr_tbl_ok(uint32_t k, uint32_t r, uint64_t sz) {
 
 struct BsrTblVariant {
     const void* fn = nullptr;
+    const void* fn_cmb = nullptr;
     char name[28] = "";
+    char name_cmb[32] = "";
 };
 BsrTblVariant g_bsr_tbl[kBsrMaxRows + 1];
 std::once_flag g_bsr_tbl_once;
 
 template <int RT>
 void fill_bsr_tbl() {
-    g_bsr_tbl[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, true, BsrTblJob>);
+    g_bsr_tbl[RT].fn = reinterpret_cast<const void*>(matapply_bsr<RT, true, false, BsrTblJob>);
+    g_bsr_tbl[RT].fn_cmb = reinterpret_cast<const void*>(matapply_bsr<RT, true, true, BsrTblJob>);
     snprintf(g_bsr_tbl[RT].name, sizeof g_bsr_tbl[RT].name, "matapply_bsr<%d,lds,tbl>", RT);
+    snprintf(g_bsr_tbl[RT].name_cmb, sizeof g_bsr_tbl[RT].name_cmb, "matapply_bsr<%d,lds,tbl,cmb>", RT);
     if constexpr (RT < kBsrMaxRows) fill_bsr_tbl<RT + 1>();
 }
 
@@ -2380,10 +2456,12 @@ hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t b
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
     job.addr = t.dev;
-    const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
-    if ((e = launch_job(g_bsr_tbl[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job)) != hipSuccess)
+    const bool cmb = bsr_cmb(nw);
+    const uint32_t ph = cmb ? bsr_cmb_phase(nw) : kBsrPhase, kp = k < ph ? k : ph;
+    if ((e = launch_job(cmb ? g_bsr_tbl[rt].fn_cmb : g_bsr_tbl[rt].fn, grid, 64 * nw,
+                        size_t(kp) * (cmb ? bsr_in_bytes<true>() : bsr_in_bytes<false>()), stream, job)) != hipSuccess)
         return e;
-    t_last_kernel = g_bsr_tbl[rt].name;
+    t_last_kernel = cmb ? g_bsr_tbl[rt].name_cmb : g_bsr_tbl[rt].name;
     return bsr_table_done(t, stream);
 }
 
@@ -2434,9 +2512,11 @@ hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
         t_last_kernel = g_bsr_var[rt].name_solo;
         return launch_job(g_bsr_var[rt].fn_solo, grid, 64, 0, stream, job);
     }
-    const uint32_t kp = k < kBsrPhase ? k : kBsrPhase;
-    t_last_kernel = g_bsr_var[rt].name;
-    return launch_job(g_bsr_var[rt].fn, grid, 64 * nw, size_t(kp) * kBsrChunk, stream, job);
+    const bool cmb = bsr_cmb(nw);
+    const uint32_t ph = cmb ? bsr_cmb_phase(nw) : kBsrPhase, kp = k < ph ? k : ph;
+    t_last_kernel = cmb ? g_bsr_var[rt].name_cmb : g_bsr_var[rt].name;
+    return launch_job(cmb ? g_bsr_var[rt].fn_cmb : g_bsr_var[rt].fn, grid, 64 * nw,
+                      size_t(kp) * (cmb ? bsr_in_bytes<true>() : bsr_in_bytes<false>()), stream, job);
 }
 
 }  // namespace
