@@ -296,18 +296,18 @@ def test_bsr_wide_equals_bsg(k, m):
 def tbl_name(r, units, k):
     """The kernel a launch of k > 32 inputs or > 40 rows takes (kernels.hip
     bsr_wide_ok / launch_bsr_tbl): the ks form for one row tile, or in row groups
-    of 8 for k >= 64 when the LDS-phase form would give fewer than 16 waves per
-    CU; else the LDS-phase table form with tiles of <= 8 rows (<= 4 for k > 64
-    and fewer than 16 waves per CU) in row groups of <= 8 tiles."""
-    tile = 4 if k > 64 and units * -(-r // 8) < 256 * 16 else 8
-    if k > 32 and (r <= 10 or (k >= 64 and units * -(-r // tile) < 256 * 16)):
-        ng = 1 if r <= 10 else -(-r // 8)
-        return "matapply_bsr<%d,ks,tbl>" % -(-r // ng)
+    of 8 for k >= 64 when the LDS-phase form would run fewer than 8 waves per CU
+    (units x row groups of 64 x waves per group); else the LDS-phase table form
+    with tiles of <= 8 rows in row groups of <= 8 tiles."""
+    tile = 8
     ng = -(-r // (8 * tile))
     rpg = -(-r // ng)
     nw = 1
     while nw * tile < rpg:
         nw *= 2
+    if k > 32 and (r <= 10 or (k >= 64 and units * ng * nw < 256 * 8)):
+        ng = 1 if r <= 10 else -(-r // 8)
+        return "matapply_bsr<%d,ks,tbl>" % -(-r // ng)
     # 8-wave workgroups share the inputs' combinations through LDS (kernels.hip bsr_cmb)
     return "matapply_bsr<%d,lds,tbl%s>" % (-(-rpg // nw), ",cmb" if nw >= 8 else "")
 
@@ -320,9 +320,10 @@ TBL_SHAPES = [(33, 50), (40, 60), (47, 60), (64, 112), (128, 150), (128, 256), (
 @pytest.mark.parametrize("k,m,sz", [(40, 60, (128 << 20) // 40), (128, 256, (64 << 20) // 128),
                                     (200, 256, 400 * 2048)])
 def test_bsr_table_form_large_launch(bsr_only, k, m, sz):
-    """Launches large enough for the LDS-phase table form (tiles of 8 rows for
-    40/60 and 128/256, tiles of 4 for 200/256 at 400 units): against the oracle
-    on sampled columns."""
+    """Launches large enough for the LDS-phase table form (tiles of <= 8 rows;
+    128/256 in two row groups and 200/256 at 400 units on 8-wave workgroups that
+    share their inputs' combinations through LDS): against the oracle on
+    sampled columns."""
     rng = np.random.default_rng(k + 3 * m)
     data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda")
     out = zfec_amd.Encoder(k, m).encode([data[i] for i in range(k)])

@@ -2323,27 +2323,29 @@ bool bsr_shape_ok(uint32_t k, uint32_t r, uint64_t sz) {
 constexpr uint32_t kBsrKsRows = 8;  // rows per group of the ks form past one tile
 constexpr uint32_t kBsrTblTile = 8;
 
-// Tile height of the table form of the LDS-phase kernel (below): 8 rows, or 4
-// for many inputs and too few units to give the CUs ~16 waves each (a wave per
-// tile per unit): 200/256 0.176 -> 0.145 ms per 64 MiB stripe; 40/60 0.051 ->
-// 0.061, so not for few inputs.
-uint32_t bsr_tbl_tile(uint32_t k, uint32_t r, uint64_t units) {
-    return k > 64 && units * ((r + kBsrTblTile - 1) / kBsrTblTile) < uint64_t(g_num_cu) * 16 ? 4u : kBsrTblTile;
-}
-
+// The table form of the LDS-phase kernel (below) runs tiles of <= 8 rows in row
+// groups of <= 8 tiles.  Round 4 used tiles of 4 for k > 64 in launches too
+// small for 16 waves per CU; with the 8-wave groups sharing their inputs'
+// combinations (bsr_cmb) a 4-row tile reads 30 LDS dwords per 4 rows and loses:
+// 160/256 0.183 ms with tiles of 4 against 0.122 with 8 (profiles/r05_bsr_wide_ab.json).
+//
 // The ks form (inputs split over the waves of a workgroup) serves k > 32 with
 // one row tile, and -- in row groups of 8, each re-reading the inputs -- launches
-// of k >= 64 whose LDS-phase form would have fewer than 16 waves per CU:
-// 200/256 0.143 -> 0.095 ms, 64/112 0.086 -> 0.080; at 16 waves per CU the
-// re-reads cost more (128/256: 0.157 -> 0.195), and 40/60 is even (0.051 / 0.053).
+// of k >= 64 whose LDS-phase form would run fewer than 8 waves per CU (units x
+// row groups x waves per group): 200/256 (164 units of 2 KiB per 64 MiB stripe,
+// 1,312 waves) 0.082 ms on ks against 0.153, 96/128 (1,368 waves) 0.053 against
+// 0.086; from there up the LDS-phase form wins: 160/256 (3,280 waves) 0.122,
+// 64/112 (4,096) 0.070 -> 0.055, 128/256 0.121 (ks: 0.195 in round 4).
 bool bsr_wide_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes) {
     if (generic_mode() != 2 || k <= static_cast<uint32_t>(kMaxIn) || k > static_cast<uint32_t>(kMaxWideIn) || r < 1 ||
         r > 256 || sz < kBsgChunk || k * r < 24)
         return false;
     if (r <= static_cast<uint32_t>(kBsrMaxRows)) return true;
     const uint64_t units = (sz + kBsrChunk - 1) / kBsrChunk * nstripes;
-    const uint32_t tile = bsr_tbl_tile(k, r, units);
-    return k >= 64 && units * ((r + tile - 1) / tile) < uint64_t(g_num_cu) * 16;
+    const uint32_t ng = (r + 8 * kBsrTblTile - 1) / (8 * kBsrTblTile), rpg = (r + ng - 1) / ng;
+    uint32_t nw = 1;  // as launch_bsr_tbl
+    while (nw * kBsrTblTile < rpg) nw *= 2;
+    return k >= 64 && units * ng * nw < uint64_t(g_num_cu) * 8;
 }
 
 struct BsrKsVariant {
@@ -2468,9 +2470,7 @@ hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t b
 hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     uint64_t base = 0;
     if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
-    const uint32_t r = a.r;
-    const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
-    const uint32_t tile = bsr_tbl_tile(a.k, r, cps * a.nstripes);
+    const uint32_t r = a.r, tile = kBsrTblTile;
     const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
     const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
     uint32_t nw = 1;                                   // 1, 2, 4 or 8 waves: see bsr_tiles
