@@ -808,7 +808,7 @@ def run_workload(k, m, sz, ns, steps, warmup, dist, use_graph=False, layout="256
 def decode_fresh(code, k, m, sz, ns, ld, data, par, recv, n, stream):
     """Decodes that each use a new random set of k received blocks: a matrix
     the process has never seen, so no specialised (JIT) kernel exists for it
-    and the launch runs on what serves first-seen patterns (matapply_bsg).
+    and the launch runs on what serves first-seen patterns (matapply_bsr).
     One launch per pattern between events (the staging copy into slot order is
     outside them); every result is checked against the stripe."""
     rng = np.random.default_rng(4321)
@@ -826,7 +826,7 @@ def decode_fresh(code, k, m, sz, ns, ld, data, par, recv, n, stream):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         code.decode_batch(recv.data_ptr(), ld, k * ld, out.data_ptr(), ld, k * ld, sl, sz, ns,
-                          stream=stream.cuda_stream)
+                          stream=stream.cuda_stream, flags=ROW_PADDING_FLAGS)
         b.record(stream)
         kern = capi.last_kernel_name()
         LEGS.add("decode fresh", kern)
@@ -850,6 +850,11 @@ def run_batched_1mib(steps):
     launch, in two layouts:
       object-major  [stripe][block][row] (rows 256-byte aligned, as in the main
                     workload): one launch walks 256 stripes of 10 rows each;
+                    with FEC_FLAG_ROW_PADDING as the main workload's calls
+                    (the headline), and without it (every output row's last
+                    128-byte line partly written: HBM completes each such line
+                    with a read-modify-write, 147 -> 161 us per launch,
+                    profiles/r05_rowend_ab.json);
       block-major   block j of every stripe back to back ([block][stripe][sz],
                     stripe stride = sz): fec_encode_batch runs it as ONE stripe
                     of 256 x sz bytes per block, 10 long streams.
@@ -864,9 +869,13 @@ def run_batched_1mib(steps):
     st = torch.cuda.current_stream()
     nums = list(range(k, m))
     res = {"shape": "K=3/M=10 encode, 256 x 1 MiB stripes per launch", "algorithmic_bytes_per_launch": m * sz * ns,
-           "layouts": {}}
-    for layout in ("object-major", "block-major"):
-        if layout == "object-major":
+           "layouts": {}, "row_padding": ("object-major: the calls carry FEC_FLAG_ROW_PADDING, as the main "
+                                          "workload's do (rows end on a whole 128-byte line inside their 256-byte "
+                                          "padding); 'object-major, rows end mid-line': the same buffers without "
+                                          "the flag (each output row's last line is written partially)")}
+    for layout in ("object-major", "object-major, rows end mid-line", "block-major"):
+        flags = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if layout == "object-major" else 0)
+        if layout.startswith("object-major"):
             fp = m * ld * ns
             shape_in, shape_out = (ns, k, ld), (ns, m - k, ld)
             sbs, sss, dbs, dss = ld, k * ld, ld, (m - k) * ld
@@ -880,7 +889,8 @@ def run_batched_1mib(steps):
 
         def enc_i(i):
             def f(sh):
-                code.encode_batch(src[i].data_ptr(), sbs, sss, dst[i].data_ptr(), dbs, dss, nums, sz, ns, stream=sh)
+                code.encode_batch(src[i].data_ptr(), sbs, sss, dst[i].data_ptr(), dbs, dss, nums, sz, ns, stream=sh,
+                                  flags=flags)
             return f
 
         warm, _ = back_to_back([enc_i(0)], steps, st, "batched_1MiB %s warm" % layout)
@@ -901,6 +911,10 @@ def run_batched_1mib(steps):
 
 
 FIRST_SEEN_PATTERNS = 5
+
+# Decode legs on the workloads' padded rows carry the same row-padding contract
+# as the timed loop (FEC_FLAG_ROW_PADDING: rows end on whole 128-byte lines).
+ROW_PADDING_FLAGS = capi.FEC_FLAG_ASYNC | capi.FEC_FLAG_ROW_PADDING
 
 
 def run_first_seen(npat=FIRST_SEEN_PATTERNS):
@@ -947,7 +961,7 @@ def run_first_seen(npat=FIRST_SEEN_PATTERNS):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         code.decode_batch(recv.data_ptr(), ld, k * ld, out.data_ptr(), ld, k * ld, sl, sz, ns,
-                          stream=stream.cuda_stream)
+                          stream=stream.cuda_stream, flags=ROW_PADDING_FLAGS)
         b.record(stream)
         kern = capi.last_kernel_name()
         LEGS.add(leg, kern)

@@ -23,8 +23,8 @@ import bench  # noqa: E402  (the tree this runs in)
 from zfec_amd import capi  # noqa: E402
 
 
-def one(ns, steps, k=3, m=10):
-    sz = -(-(1 << 20) // k)
+def one(ns, steps, k=3, m=10, flags=capi.FEC_FLAG_ASYNC, sz=None):
+    sz = sz or -(-(1 << 20) // k)
     ld = bench.row_stride(sz)
     code = capi.Code(k, m)
     st = torch.cuda.current_stream()
@@ -37,7 +37,7 @@ def one(ns, steps, k=3, m=10):
     def enc_i(i):
         def f(sh):
             code.encode_batch(src[i].data_ptr(), ld, k * ld, dst[i].data_ptr(), ld, (m - k) * ld, nums, sz, ns,
-                              stream=sh)
+                              stream=sh, flags=flags)
         return f
 
     enc_i(0)(st.cuda_stream)
@@ -52,7 +52,7 @@ def one(ns, steps, k=3, m=10):
     hbm = lambda ms: ns * m * sz / (ms * 1e-3) / 1e9
     del src, dst
     torch.cuda.empty_cache()
-    return {"stripes": ns, "kernel": kern, "nsets": nsets, "ms_cold": round(cold, 4), "ms_warm": round(warm, 4),
+    return {"stripes": ns, "sz": sz, "kernel": kern, "nsets": nsets, "ms_cold": round(cold, 4), "ms_warm": round(warm, 4),
             "frac_cold": round(hbm(cold) / bench.HBM_PEAK_GBPS, 4), "frac_warm": round(hbm(warm) / bench.HBM_PEAK_GBPS, 4)}
 
 
@@ -61,11 +61,15 @@ def main():
     ap.add_argument("--stripes", default="256,1024")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--sz", type=int, default=0, help="block size (default: a third of 1 MiB, 349,526 bytes)")
+    ap.add_argument("--row-padding", action="store_true", help="pass FEC_FLAG_ROW_PADDING (rows run to their next 128-byte line)")
     args = ap.parse_args()
     rows = []
     for rnd in range(args.rounds):
         for ns in map(int, args.stripes.split(",")):
-            r = one(ns, args.steps)
+            r = one(ns, args.steps, flags=capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if args.row_padding else 0),
+                    sz=args.sz or None)
+            r["row_padding"] = args.row_padding
             r["round"] = rnd
             rows.append(r)
             print(json.dumps(r), file=sys.stderr, flush=True)
