@@ -269,6 +269,33 @@ def test_bsr_wide_table_ring_reuse(bsr_only):
         assert (torch.stack(got).cpu().numpy() == data).all(), nums
 
 
+def test_bsr_table_cache_cross_stream(bsr_only):
+    """A matrix's routine-address table is uploaded once, on the stream of its
+    first launch (kernels.hip bsr_addr_table); a launch of the same matrix on
+    another stream must wait for that upload.  The first stream is held by a
+    spin kernel while the second launch is queued, so a missing wait would
+    run the second kernel on an empty table."""
+    k, m, sz = 94, 100, 8192
+    rng = np.random.default_rng(942)
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    want = oracle.encode(k, m, data)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    enc = zfec_amd.Encoder(k, m)
+    outs = []
+    for rep in range(3):
+        with torch.cuda.stream(s1):
+            torch.cuda._sleep(5_000_000)  # the upload on s1 waits behind this
+            outs.append(enc.encode(ins)[k:])
+        with torch.cuda.stream(s2):
+            outs.append(enc.encode(ins)[k:])
+    torch.cuda.synchronize()
+    assert capi.last_kernel_name() == "matapply_bsr<6,ks,tbl>", capi.last_kernel_name()
+    for o in outs:
+        assert (torch.stack(o).cpu().numpy() == want).all()
+
+
 @pytest.mark.parametrize("k,m", [(94, 100), (255, 256)])
 def test_bsr_wide_equals_bsg(k, m):
     """Generic mode 2 (matapply_bsr_ks) and 1 (matapply_bsg's table form) on the

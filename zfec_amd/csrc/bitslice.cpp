@@ -323,8 +323,12 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     auto launder = [&](const char* indent) {
         e("%sKArgs ka = ka0;\n%sasm volatile(\"\" : \"+s\"(ka));\n", indent, indent);
     };
+    // share: the unit's inputs go through LDS in phases of `ph` (all k at once
+    // when opt.phase is 0): a phase's inputs are loaded and transposed once,
+    // by the waves in turn, then every wave applies them to its tile
+    const unsigned ph = split && opt.share ? (opt.phase && opt.phase < k ? opt.phase : k) : 0;
     if (split && opt.share) {
-        e("  __shared__ u32x4 sh[%u];  // [input][half][lane] bit-planes of the unit\n", k * 128);
+        e("  __shared__ u32x4 sh[%u];  // [input of the phase][half][lane] bit-planes\n", ph * 128);
         e("  const u32 lane = threadIdx.x & 63u;\n");
     }
     if (split) {
@@ -355,7 +359,8 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     auto emit_load = [&](unsigned n) {
         const unsigned j = n % k;
         if (share) {
-            e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, j * 128, n, j * 128 + 64);
+            const unsigned sl = j % ph;  // slot of input j in its phase
+            e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, sl * 128, n, sl * 128 + 64);
             return;
         }
         char dst[16], rsrc[16];
@@ -366,32 +371,27 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     };
     if (!split)
         for (unsigned n = 0; n < pf && n < nsteps; ++n) emit_load(n);
-    if (share) {
-        e("    // inputs -> bit-planes -> LDS, k / %u per wave\n", ntiles);
-        for (unsigned t = 0; t < ntiles; ++t) {
-            if (t >= k) break;
-            e("    if (tile == %uu) {\n", t);
-            launder("      ");
-            for (unsigned j = t; j < k; j += ntiles) {
-                char dst[16], rsrc[16];
-                snprintf(dst, sizeof dst, "p%u", j);
-                snprintf(rsrc, sizeof rsrc, "pi%u", j);
-                e("      const __amdgpu_buffer_rsrc_t pi%u = %s(%sin[%u] + ub);\n", j, RS, PA, j);
-                emit_ld("      ", dst, rsrc, j);
-            }
-            for (unsigned j = t; j < k; j += ntiles) {
-                e("      u32 w%u_0 = p%u_0.x, w%u_1 = p%u_0.y, w%u_2 = p%u_0.z, w%u_3 = p%u_0.w;\n", j, j, j, j, j, j, j,
-                  j);
-                e("      u32 w%u_4 = p%u_1.x, w%u_5 = p%u_1.y, w%u_6 = p%u_1.z, w%u_7 = p%u_1.w;\n", j, j, j, j, j, j, j,
-                  j);
-                e("      tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
-                e("      sh[%uu + lane] = u32x4{w%u_0, w%u_1, w%u_2, w%u_3};\n", j * 128, j, j, j, j);
-                e("      sh[%uu + lane] = u32x4{w%u_4, w%u_5, w%u_6, w%u_7};\n", j * 128 + 64, j, j, j, j);
-            }
-            e("    }\n");
+    // The load stage of phase [j0, j1) for the wave of tile t: inputs
+    // j0 + t, j0 + t + ntiles, ... -> bit-planes -> LDS, then a barrier.  Every
+    // tile branch runs the same phases, so the waves meet at the same barriers.
+    auto emit_phase_load = [&](unsigned t, unsigned j0, unsigned j1) {
+        e("    // inputs %u..%u -> bit-planes -> LDS, one in %u per wave\n", j0, j1 - 1, ntiles);
+        for (unsigned j = j0 + t; j < j1; j += ntiles) {
+            char dst[16], rsrc[16];
+            snprintf(dst, sizeof dst, "p%u", j);
+            snprintf(rsrc, sizeof rsrc, "pi%u", j);
+            e("    const __amdgpu_buffer_rsrc_t pi%u = %s(%sin[%u] + ub);\n", j, RS, PA, j);
+            emit_ld("    ", dst, rsrc, j);
+        }
+        for (unsigned j = j0 + t; j < j1; j += ntiles) {
+            e("    u32 w%u_0 = p%u_0.x, w%u_1 = p%u_0.y, w%u_2 = p%u_0.z, w%u_3 = p%u_0.w;\n", j, j, j, j, j, j, j, j);
+            e("    u32 w%u_4 = p%u_1.x, w%u_5 = p%u_1.y, w%u_6 = p%u_1.z, w%u_7 = p%u_1.w;\n", j, j, j, j, j, j, j, j);
+            e("    tr8(w%u_0, w%u_1, w%u_2, w%u_3, w%u_4, w%u_5, w%u_6, w%u_7);\n", j, j, j, j, j, j, j, j);
+            e("    sh[%uu + lane] = u32x4{w%u_0, w%u_1, w%u_2, w%u_3};\n", (j - j0) * 128, j, j, j, j);
+            e("    sh[%uu + lane] = u32x4{w%u_4, w%u_5, w%u_6, w%u_7};\n", (j - j0) * 128 + 64, j, j, j, j);
         }
         e("    __syncthreads();\n");
-    }
+    };
     for (unsigned t = 0; t < ntiles; ++t) {
         const unsigned r0 = tile_lo[t], r1 = tile_lo[t + 1];
         const unsigned seq_end = split ? (t + 1) * k : nsteps;  // prefetch horizon
@@ -399,14 +399,27 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         if (split) {
             e("    if (tile == %uu) {\n", t);
             launder("    ");
-            for (unsigned n = t * k; n < t * k + pf && n < seq_end; ++n) emit_load(n);
+            if (!share)
+                for (unsigned n = t * k; n < t * k + pf && n < seq_end; ++n) emit_load(n);
         }
         std::vector<char> init(size_t(r1 - r0) * 8, 0);
         for (unsigned i = r0; i < r1; ++i)
             e("    u32 a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7;\n", i, i, i, i, i, i, i, i);
         for (unsigned j = 0; j < k; ++j) {
             const unsigned n = t * k + j;
-            if (pf == 0)
+            if (share) {
+                // LDS reads pf steps ahead inside the phase; the phase's load stage first
+                const unsigned pe = (j / ph + 1) * ph < k ? (j / ph + 1) * ph : k;  // end of j's phase
+                if (j % ph == 0) {
+                    if (j) e("    __syncthreads();  // the previous phase's planes are read\n");
+                    emit_phase_load(t, j, pe);
+                    for (unsigned x = j; x < j + pf && x < pe; ++x) emit_load(t * k + x);
+                }
+                if (pf == 0)
+                    emit_load(n);
+                else if (j + pf < pe)
+                    emit_load(n + pf);
+            } else if (pf == 0)
                 emit_load(n);
             else if (n + pf < seq_end)
                 emit_load(n + pf);
@@ -670,10 +683,18 @@ void run_compile(Entry* e, std::string src) {
 std::atomic<int> g_mode{-1};
 
 // Options of a kernel for an r x k matrix: the configured ones, with the
-// planes shared through LDS only while all k inputs' planes fit (2 KiB each).
-BsOptions options_for(unsigned k) {
+// planes shared through LDS only while all k inputs' planes fit (2 KiB each),
+// and in phases of 8 inputs where all k at once would cap the residency below
+// what the kernel's registers allow (~3 waves per SIMD, i.e. 12 / tiles
+// workgroups per CU): the r = 20 decode of K=20/M=60 (2 tiles, 40 KiB: 2 waves
+// per SIMD) 0.672-0.694 -> 0.686-0.713 of HBM; its r = 40 encode (4 tiles,
+// register-bound either way) loses 0.678-0.691 -> 0.665 with phases, so keeps
+// all inputs (profiles/r05_jit_phase_ab.json).
+BsOptions options_for(unsigned k, unsigned r) {
     BsOptions o;
     if (k > 32) o.share = false;
+    const unsigned nt = bitslice_tiles(r, o);
+    o.phase = k * 2u * 12u > 160u * nt ? 8u : 0u;
     return o;
 }
 
@@ -688,7 +709,10 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     snprintf(hdr, sizeof hdr, "%u/%u/%u/%u/1/2/0/0/%d/", k, r, opt.max_tile, opt.prefetch, opt.split ? 1 : 0);
     key += hdr;
     key += "argload/shift64/";
-    if (opt.share && bitslice_split(r, opt)) key += "share/";
+    if (opt.share && bitslice_split(r, opt)) {
+        key += "share/";
+        if (opt.phase && opt.phase < k) key += "phase" + std::to_string(opt.phase) + "/";
+    }
     if (bitslice_ksplit(k, r, opt)) key += "ksplit/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);
     return key;
@@ -696,7 +720,7 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
 
 Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
     Registry& R = reg();
-    const BsOptions opt = options_for(k);
+    const BsOptions opt = options_for(k, r);
     const std::string key = entry_key(coef, k, r, opt);
     auto it = R.entries.find(key);
     if (it != R.entries.end()) return it->second.get();
@@ -831,7 +855,7 @@ hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const cha
         Registry& R = reg();
         std::unique_lock<std::mutex> lk(R.mu);
         if (mode == kJitAuto) {
-            const std::string key = entry_key(coef, k, r, options_for(k));
+            const std::string key = entry_key(coef, k, r, options_for(k, r));
             if (!R.entries.count(key)) {
                 if (R.entries.size() >= kAutoMaxKernels) return hipErrorNotSupported;
                 if (R.seen.size() > 4 * kAutoMaxKernels) R.seen.clear();
