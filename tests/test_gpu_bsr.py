@@ -444,3 +444,52 @@ def test_bsr_past_grid_cap(bsr_only, k, m, sz, ns):
         assert (got == oracle.encode(k, m, data[s].cpu().numpy())).all(), s
         want_rec = oracle.decode(k, m, rv[s].cpu().numpy(), sl)
         assert (rec[s].cpu().numpy() == want_rec).all(), s
+
+
+# Routine addresses travel in the kernel arguments up to 432 of them (kernels.hip
+# kBsrArgAddrs: waves x inputs x rows per wave), past that in the cached
+# device-side table: 27/43 (2 waves x 27 inputs x 8 rows = 432) and 28/44 (448)
+# sit on either side; 20/60 encodes 40 rows (4 x 20 x 10 = 800, the table form).
+@pytest.mark.parametrize("k,m,want", [(27, 43, "matapply_bsr<8,lds>"), (28, 44, "matapply_bsr<8,lds,tbl>"),
+                                      (20, 60, "matapply_bsr<10,lds,tbl>")])
+def test_bsr_argument_and_table_forms(bsr_only, k, m, want):
+    rng = np.random.default_rng(k * 7 + m)
+    for sz in (2048, 5000, 9000):
+        data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+        ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+        out = zfec_amd.Encoder(k, m).encode(ins)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name() == want, (sz, capi.last_kernel_name())
+        assert (torch.stack(out[k:]).cpu().numpy() == oracle.encode(k, m, data)).all(), sz
+
+
+@pytest.mark.parametrize("k,m", [(94, 100), (20, 60), (20, 40)])
+def test_bsr_graph_capture(bsr_only, k, m):
+    """Encodes captured into a HIP graph and replayed: the table forms (device-
+    side tables the host fills at enqueue time) decline under capture
+    (kernels.hip stream_capturing) and a kernel described wholly by its
+    arguments serves; replays and a later eager launch of the same matrix (whose
+    address table must not be a slot whose upload was only recorded) are
+    bit-exact."""
+    rng = np.random.default_rng(k * 31 + m)
+    sz = 9000
+    data = rng.integers(0, 256, size=(k, sz), dtype=np.uint8)
+    want = oracle.encode(k, m, data)
+    ins = [torch.from_numpy(data[i]).cuda() for i in range(k)]
+    enc = zfec_amd.Encoder(k, m)
+    enc.encode(ins)  # warm-up outside the capture (first launch of the matrix, probe)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out = enc.encode(ins)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        assert (torch.stack(out[k:]).cpu().numpy() == want).all()
+    eager = enc.encode(ins)
+    torch.cuda.synchronize()
+    assert (torch.stack(eager[k:]).cpu().numpy() == want).all()

@@ -314,8 +314,10 @@ int apply_matrix_range(const uint8_t* coef, unsigned coef_stride, unsigned k, un
     const size_t cps = (sz + kMinChunk - 1) / kMinChunk;
     const size_t stripes_per_launch = std::max<size_t>(1, config().launch_units / cps);
     // wide codes: every input in one bit-sliced pass per row group
+    // (not under graph capture: the one-pass wide kernels read device-side
+    // tables filled at enqueue time; the passes' kernels take their arguments)
     const bool wide = k > static_cast<unsigned>(kMaxIn) &&
-                      wide_launch_ok(k, r, sz, std::min(stripes_per_launch, nstripes));
+                      wide_launch_ok(k, r, sz, std::min(stripes_per_launch, nstripes)) && !stream_capturing(stream);
     const unsigned kstep = wide ? k : static_cast<unsigned>(kMaxIn);
     const uint8_t* pin[kMaxWideIn];
     uint8_t* pout[kMaxWideIn];

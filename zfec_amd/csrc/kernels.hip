@@ -1995,6 +1995,12 @@ hipError_t ring_slot(TableRing** ring, unsigned* slot) {
     return hipSuccess;
 }
 
+// Whether `stream` is being captured into a HIP graph.  The table forms read a
+// device-side table the host fills (and reuses) at enqueue time: a captured
+// graph would replay its copy from a host slot rewritten since, and the bsr
+// address cache would hold a slot whose upload never ran (the copy is only
+// recorded).  Under capture those forms decline (hipErrorNotSupported) and a
+// kernel whose whole description travels in its arguments takes the launch.
 hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsg_once, [] { fill_bsg<0>(); });
     const uint32_t k = a.k, r = a.r;
@@ -2055,6 +2061,7 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
         return launch_job(v.fn_karg, grid, 256, lds, stream, job);
     }
     // pointers and coefficients in a device-side table
+    if (stream_capturing(stream)) return hipErrorNotSupported;
     const size_t bytes = 8 * size_t(k + r) + walk;
     if (bytes > TableRing::kSlotBytes) return hipErrorNotSupported;
     TableRing* ring = nullptr;
@@ -2126,14 +2133,18 @@ void fill_bsr() {
 constexpr int kBsrMaxDevices = 64;
 struct BsrBase {
     std::once_flag once;
+    std::atomic<bool> known{false};  // the probe has run (addr 0: it failed)
     uint64_t addr = 0;
 };
 BsrBase g_bsr_base[kBsrMaxDevices];
 
-hipError_t bsr_routine_base(uint64_t* base) {
+hipError_t bsr_routine_base(uint64_t* base, hipStream_t stream) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kBsrMaxDevices) return hipErrorNotSupported;
     BsrBase& b = g_bsr_base[dev];
+    // the probe synchronises a stream of its own: not while the launch stream is
+    // being captured into a graph (the launch declines; a later one probes)
+    if (!b.known.load(std::memory_order_acquire) && stream_capturing(stream)) return hipErrorNotSupported;
     std::call_once(b.once, [&b] {
         hipStream_t st = nullptr;
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
@@ -2145,6 +2156,7 @@ hipError_t bsr_routine_base(uint64_t* base) {
             (void)hipHostFree(h);
         }
         (void)hipStreamDestroy(st);
+        b.known.store(true, std::memory_order_release);
     });
     if (!b.addr) return hipErrorNotSupported;
     *base = b.addr;
@@ -2243,7 +2255,7 @@ hipError_t bsr_addr_table(const ApplySpec& a, hipStream_t stream, uint64_t base,
                           uint32_t split, BsrTblRef* ref) {
     const uint32_t k = a.k, r = a.r;
     const size_t n = size_t(ng) * nw * k * rt;
-    if (n * 8 > BsrTblCache::kSlotBytes) return hipErrorNotSupported;
+    if (n * 8 > BsrTblCache::kSlotBytes || stream_capturing(stream)) return hipErrorNotSupported;
     int devid = 0;
     hipError_t e = hipGetDevice(&devid);
     if (e != hipSuccess) return e;
@@ -2365,7 +2377,7 @@ void fill_bsr_ks() {
 hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_ks_once, [] { fill_bsr_ks<1>(); });
     uint64_t base = 0;
-    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
+    if (bsr_routine_base(&base, stream) != hipSuccess) return hipErrorNotSupported;
     const uint32_t k = a.k, r = a.r;
     const uint32_t ng = r <= static_cast<uint32_t>(kBsrMaxRows) ? 1u : (r + kBsrKsRows - 1) / kBsrKsRows;
     const uint32_t rt = (r + ng - 1) / ng;
@@ -2469,7 +2481,7 @@ hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t b
 
 hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     uint64_t base = 0;
-    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
+    if (bsr_routine_base(&base, stream) != hipSuccess) return hipErrorNotSupported;
     const uint32_t r = a.r, tile = kBsrTblTile;
     const uint32_t ng = (r + 8 * tile - 1) / (8 * tile);  // row groups of <= 8 waves
     const uint32_t rpg = (r + ng - 1) / ng;            // rows of the largest group
@@ -2481,7 +2493,7 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_once, [] { fill_bsr<1>(); });
     uint64_t base = 0;
-    if (bsr_routine_base(&base) != hipSuccess) return hipErrorNotSupported;
+    if (bsr_routine_base(&base, stream) != hipSuccess) return hipErrorNotSupported;
     const uint32_t k = a.k, r = a.r;
     const uint64_t cps = (a.sz + kBsrChunk - 1) / kBsrChunk;
     const uint64_t units = cps * a.nstripes;
@@ -2549,6 +2561,11 @@ void matapply_request_signal(uint32_t* flag_dev, uint32_t seq) {
 
 bool matapply_signal_used() { return t_signal_used; }
 
+bool stream_capturing(hipStream_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
 bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes) {
     // (forced) a specialised kernel of the whole matrix
     if (jit_mode() == kJitForce && sz >= static_cast<uint64_t>(kBsChunk) && k * r <= kJitMaxCoef) return true;
@@ -2611,7 +2628,10 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream) {
             e = launch_bsr_tbl(a, stream);
         if (e != hipErrorNotSupported) return e;
     }
-    if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) return launch_bsg(a, stream);
+    if (!a.accumulate && bsg_shape_ok(k, r, a.sz)) {
+        const hipError_t e = launch_bsg(a, stream);
+        if (e != hipErrorNotSupported) return e;  // (its table form declines under graph capture)
+    }
     if (reg && !a.accumulate) return g_reg_launch[k][r](a, stream, sig);
     return launch_lds(a, stream);
 }

@@ -67,6 +67,14 @@ hipError_t launch_apply(const ApplySpec& a, hipStream_t stream);
 // caller launches them one at a time).  Neither may read what the other writes.
 hipError_t launch_apply_pair(const ApplySpec& x, const ApplySpec& y, hipStream_t stream);
 
+// Whether `stream` is being captured into a HIP graph.  The table forms (a
+// device-side table the host fills and reuses at enqueue time) decline then:
+// a captured graph would replay copies from host slots rewritten since, or
+// read a cached device table whose upload was only recorded.  launch_apply
+// falls back to kernels whose whole description travels in their arguments;
+// wide launches (k > kMaxIn) are split into passes by the caller.
+bool stream_capturing(hipStream_t stream);
+
 // Whether launch_apply takes all k > kMaxIn inputs of a launch of r <= kMaxOut
 // rows, sz-byte blocks and nstripes stripes in one pass (bit-sliced kernels).
 bool wide_launch_ok(uint32_t k, uint32_t r, uint64_t sz, uint64_t nstripes);
