@@ -9,8 +9,9 @@ Strategies timed (GB/s of stripe input bytes, 1e9):
                  after zfec_amd.reuse_host_memory()
   pinned_api     the same C-ABI call with pinned (hipHostMalloc'd) host buffers,
                  e.g. a reader that reads file/socket data straight into pinned
-                 memory: the library DMAs them in chunks, overlapping H2D,
-                 kernel and D2H
+                 memory: the kernel reads and writes them in place over PCIe
+                 (zero-copy, both link directions at once; run_single in
+                 zfec_amd/csrc/fec_abi.cpp)
   bytes_call     the library call alone: the previous call's output bytes are
                  still alive while the next call runs (their free is outside
                  the timing), after zfec_amd.reuse_host_memory()

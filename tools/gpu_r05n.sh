@@ -1,13 +1,19 @@
-# round 5, session n: wide codes with many rows on the LDS-phase form with shared
-# combinations (var1: every k > 32, r > 10 launch on lds,tbl; var2: the same
-# with 8-row tiles always) against the shipped ks row groups
+# round 5, session n: inputs per LDS phase of matapply_bsr's plane-sharing form
+# as a launch field (bsr_phase: 5 nw inputs at most, equal phases; cfg4's
+# 20-input first-seen decodes 10 + 10 instead of 8 + 8 + 4) against the previous
+# tree (scratch/base, phases of 8) and var1 (at most 4 nw: 7 + 7 + 6); parity first
 set -o pipefail
 O=gpurun_out/r05n
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_bsr.py \
+  > $O/pytest_bsr.log 2>&1 || { echo pytest-failed; tail -30 $O/pytest_bsr.log; exit 1; }
+tail -2 $O/pytest_bsr.log
 for i in 1 2; do
-  for t in new var1 var2; do
+  for t in new base var1; do
     if [ $t = new ]; then d=.; else d=scratch/$t; fi
-    (cd $d && timeout -k 10 400 python -u tools/wide_bench.py --shapes 200/256,64/112,160/256,100/200,128/256 --variants generic --launches 10) \
+    (cd $d && timeout -k 10 300 python -u bench.py --workload first_seen) > $O/fs_${t}_$i.json 2> $O/fs_${t}_$i.err \
+      || { echo fs-$t-failed; tail -20 $O/fs_${t}_$i.err; exit 1; }
+    (cd $d && timeout -k 10 400 python -u tools/wide_bench.py --shapes 20/40,20/60,12/30,30/70 --variants generic --launches 10) \
       > $O/wide_${t}_$i.json 2> $O/wide_${t}_$i.err || { echo wide-$t-failed; tail -20 $O/wide_${t}_$i.err; exit 1; }
   done
 done
