@@ -1139,6 +1139,13 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
 constexpr int kBsrBatch = 4;          // inputs a wave loads at once
 constexpr uint32_t kBsrPhase = 8;     // inputs whose planes share LDS at a time (multi-wave form)
+// Wave priority of the plane-sharing table form's load stage (s_setprio while a
+// wave loads and transposes a phase's inputs, 0 for its routine calls): one
+// 64 MiB stripe of 30/70 0.070-0.072 -> 0.068-0.069 ms encode, 0.063-0.064 ->
+// 0.061 decode.  The other forms keep one priority: cfg4's first-seen decodes
+// (argument form) 0.430 -> 0.433-0.435 ms with it, 128/256 (combination
+// sharing) 0.121 -> 0.125 (160/256 0.123 -> 0.120); profiles/r05_bsr_prio_ab.json.
+constexpr int kBsrTblLoadPrio = 3;
 // Inputs per phase of the combination-sharing form (7.5 KiB each): one per wave,
 // so the 16 / nw workgroups a CU holds at 4 waves per SIMD take 120 KiB.
 __host__ __device__ constexpr uint32_t bsr_cmb_phase(uint32_t nw) { return nw; }
@@ -1281,6 +1288,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         for (uint32_t ph = 0; ph < k; ph += kp) {
             const uint32_t kn = k - ph < kp ? k - ph : kp;
             // inputs -> bit-planes -> LDS, inputs wave, wave + nw, ... in batches
+            if constexpr (TBL && !CMB) __builtin_amdgcn_s_setprio(kBsrTblLoadPrio);
             for (uint32_t j0 = wave; j0 < kn; j0 += kBat * nw) {
                 u32x4 x[kBat][2];
 #pragma unroll
@@ -1313,6 +1321,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
                     }
                 }
             }
+            if constexpr (TBL && !CMB) __builtin_amdgcn_s_setprio(0);
             __syncthreads();
             // the phase's inputs in pairs with fixed address registers (A: even,
             // B: odd): after input j's calls its set is reloaded (scalar loads,
