@@ -67,7 +67,7 @@ struct Src {
     }
 };
 
-const char* const kPrelude = R"(typedef unsigned int u32;
+const char* const kPrelude = R"PRE(typedef unsigned int u32;
 typedef unsigned long long u64;
 typedef unsigned char u8;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
@@ -135,7 +135,15 @@ __device__ __forceinline__ u32x4 ld(__amdgpu_buffer_rsrc_t r, u32 off) {
 __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, u32 off, u32x4 v) {
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
 }
-)";
+// LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes at p land at lds + 16 l
+typedef __attribute__((address_space(1))) void GV;
+typedef __attribute__((address_space(3))) void LV;
+__device__ __forceinline__ void dma16(const u8* p, u32x4* lds) {
+    __builtin_amdgcn_global_load_lds((const GV*)p, (LV*)lds, 16, 0, 0);
+}
+// the LDS-DMA writes have landed (hipcc orders no LDS read after them itself)
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+)PRE";
 
 // Name of the XOR of input planes {base + a : bit a of m} of step n (m != 0),
 // emitting the combinations it needs on first use.
@@ -327,8 +335,13 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // when opt.phase is 0): a phase's inputs are loaded and transposed once,
     // by the waves in turn, then every wave applies them to its tile
     const unsigned ph = split && opt.share ? (opt.phase && opt.phase < k ? opt.phase : k) : 0;
+    // dma: a phase's inputs go straight into LDS (LDS-DMA) and are transposed
+    // in place; with more than one phase, two are resident and the next one
+    // loads while the waves walk the current one (db)
+    const bool db = split && opt.share && opt.dma && ph < k;
+    const bool dma = db;
     if (split && opt.share) {
-        e("  __shared__ u32x4 sh[%u];  // [input of the phase][half][lane] bit-planes\n", ph * 128);
+        e("  __shared__ u32x4 sh[%u];  // [buffer][input of the phase][half][lane] bit-planes\n", (db ? 2 : 1) * ph * 128);
         e("  const u32 lane = threadIdx.x & 63u;\n");
     }
     if (split) {
@@ -356,11 +369,12 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     auto emit_ld = [&](const char* ind, const char* dst, const char* rsrc, unsigned) {
         e("%sconst u32x4 %s_0 = ld(%s, lo16), %s_1 = ld(%s, lo16 + 1024u);\n", ind, dst, rsrc, dst, rsrc);
     };
+    auto phase_base = [&](unsigned j) { return db ? (j / ph) % 2 * ph * 128 : 0u; };  // u32x4 offset of j's buffer
     auto emit_load = [&](unsigned n) {
         const unsigned j = n % k;
         if (share) {
-            const unsigned sl = j % ph;  // slot of input j in its phase
-            e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, sl * 128, n, sl * 128 + 64);
+            const unsigned sl = phase_base(j) + j % ph * 128;  // slot of input j in its phase's buffer
+            e("    const u32x4 l%u_0 = sh[%uu + lane], l%u_1 = sh[%uu + lane];\n", n, sl, n, sl + 64);
             return;
         }
         char dst[16], rsrc[16];
@@ -374,7 +388,34 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
     // The load stage of phase [j0, j1) for the wave of tile t: inputs
     // j0 + t, j0 + t + ntiles, ... -> bit-planes -> LDS, then a barrier.  Every
     // tile branch runs the same phases, so the waves meet at the same barriers.
+    // LDS-DMA of phase [j0, j1)'s inputs of the wave of tile t into its buffer,
+    // and (after the wait) their in-place transposes
+    auto emit_dma = [&](unsigned t, unsigned j0, unsigned j1) {
+        e("    // inputs %u..%u -> LDS (DMA), one in %u per wave\n", j0, j1 - 1, ntiles);
+        for (unsigned j = j0 + t; j < j1; j += ntiles) {
+            const unsigned sl = phase_base(j) + (j - j0) * 128;
+            e("    dma16(%sin[%u] + ub + lo16, sh + %uu);\n", PA, j, sl);
+            e("    dma16(%sin[%u] + ub + lo16 + 1024u, sh + %uu);\n", PA, j, sl + 64);
+        }
+    };
+    auto emit_xpose = [&](unsigned t, unsigned j0, unsigned j1) {
+        e("    dma_wait();  // inputs %u..%u -> bit-planes in place\n", j0, j1 - 1);
+        for (unsigned j = j0 + t; j < j1; j += ntiles) {
+            const unsigned sl = phase_base(j) + (j - j0) * 128;
+            e("    {\n      const u32x4 y0 = sh[%uu + lane], y1 = sh[%uu + lane];\n", sl, sl + 64);
+            e("      u32 w0 = y0.x, w1 = y0.y, w2 = y0.z, w3 = y0.w, w4 = y1.x, w5 = y1.y, w6 = y1.z, w7 = y1.w;\n");
+            e("      tr8(w0, w1, w2, w3, w4, w5, w6, w7);\n");
+            e("      sh[%uu + lane] = u32x4{w0, w1, w2, w3};\n      sh[%uu + lane] = u32x4{w4, w5, w6, w7};\n    }\n", sl,
+              sl + 64);
+        }
+    };
     auto emit_phase_load = [&](unsigned t, unsigned j0, unsigned j1) {
+        if (dma) {
+            emit_dma(t, j0, j1);
+            emit_xpose(t, j0, j1);
+            e("    __syncthreads();\n");
+            return;
+        }
         e("    // inputs %u..%u -> bit-planes -> LDS, one in %u per wave\n", j0, j1 - 1, ntiles);
         for (unsigned j = j0 + t; j < j1; j += ntiles) {
             char dst[16], rsrc[16];
@@ -405,12 +446,22 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
         std::vector<char> init(size_t(r1 - r0) * 8, 0);
         for (unsigned i = r0; i < r1; ++i)
             e("    u32 a%u_0, a%u_1, a%u_2, a%u_3, a%u_4, a%u_5, a%u_6, a%u_7;\n", i, i, i, i, i, i, i, i);
+        if (db) {  // the first phase's inputs (its barrier opens the phase loop)
+            emit_dma(t, 0, ph);
+            emit_xpose(t, 0, ph);
+        }
         for (unsigned j = 0; j < k; ++j) {
             const unsigned n = t * k + j;
             if (share) {
                 // LDS reads pf steps ahead inside the phase; the phase's load stage first
                 const unsigned pe = (j / ph + 1) * ph < k ? (j / ph + 1) * ph : k;  // end of j's phase
-                if (j % ph == 0) {
+                if (j % ph == 0 && db) {
+                    // phase [j, pe)'s planes are in; every wave has walked the previous
+                    // phase, whose buffer the next phase's DMA now overwrites
+                    e("    __syncthreads();\n");
+                    if (pe < k) emit_dma(t, pe, pe + ph < k ? pe + ph : k);
+                    for (unsigned x = j; x < j + pf && x < pe; ++x) emit_load(t * k + x);
+                } else if (j % ph == 0) {
                     if (j) e("    __syncthreads();  // the previous phase's planes are read\n");
                     emit_phase_load(t, j, pe);
                     for (unsigned x = j; x < j + pf && x < pe; ++x) emit_load(t * k + x);
@@ -457,6 +508,8 @@ std::string bitslice_source(const uint8_t* coef, unsigned k, unsigned r, const B
             for (const Upd& u : ups)
                 update(u, u.ml ? lo.name(u.ml, e) : std::string(), u.mh ? hi.name(u.mh, e) : std::string());
             e("    __builtin_amdgcn_sched_barrier(0);\n");
+            if (db && (j + 1) % ph == 0 && j + 1 < k)  // the last input of a phase: the next one's planes
+                emit_xpose(t, j + 1, j + 1 + ph < k ? j + 1 + ph : k);
         }
         for (unsigned i = r0; i < r1; ++i) {
             for (unsigned b = 0; b < 8; ++b)
@@ -694,7 +747,8 @@ BsOptions options_for(unsigned k, unsigned r) {
     BsOptions o;
     if (k > 32) o.share = false;
     const unsigned nt = bitslice_tiles(r, o);
-    o.phase = k * 2u * 12u > 160u * nt ? 8u : 0u;
+    o.phase = k * 2u * 12u > 160u * nt ? 4u : 0u;
+    o.dma = o.phase && o.phase < k;
     return o;
 }
 
@@ -712,6 +766,7 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     if (opt.share && bitslice_split(r, opt)) {
         key += "share/";
         if (opt.phase && opt.phase < k) key += "phase" + std::to_string(opt.phase) + "/";
+        if (opt.dma && opt.phase && opt.phase < k) key += "dma/";
     }
     if (bitslice_ksplit(k, r, opt)) key += "ksplit/";
     key.append(reinterpret_cast<const char*>(coef), size_t(k) * r);

@@ -41,6 +41,7 @@ struct BsOptions {
     bool split = true;               // one wave per row tile of a unit (a workgroup shares the unit's inputs)
     bool share = true;               // split: inputs transposed once per unit, bit-planes shared through LDS
     unsigned phase = 8;              // share: inputs per LDS phase (0: all k at once, k x 2 KiB of LDS)
+    bool dma = true;                 // share: inputs loaded with LDS-DMA, several phases double-buffered
     bool ksplit = true;              // one row tile and k > 32: a unit's inputs split over the 4 waves of a
                                      // workgroup, partial planes reduced through LDS (4x the waves per unit)
 };

@@ -1127,28 +1127,26 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 //   matapply_bsr_solo<RT> (one tile, r <= 10): one wave per unit, no LDS; the
 //       wave loads and transposes its inputs two ahead;
 //   matapply_bsr<RT> ("lds", r > 10): one workgroup per unit, a wave per
-//       tile; phases of kBsrPhase inputs: the waves load and transpose a
-//       phase's inputs into LDS planes (16 KiB), then each walks them for its
-//       tile.  All k inputs in LDS at once (k * 2 KiB) capped the workgroups
-//       per CU and measured 0.51 ms against 0.37-0.38 with phases of 8 on
-//       cfg4's first-seen decodes (profiles/r04_bsr_ab.json).
+//       tile; the unit's inputs go through LDS in phases, loaded straight into
+//       LDS (LDS-DMA) and transposed in place into bit-planes, two phases
+//       resident so the next phase loads while the waves walk the current one
+//       (bsr_db_phase).  All k inputs in LDS at once (k * 2 KiB) capped the
+//       workgroups per CU and measured 0.51 ms against 0.37-0.38 with phases
+//       of 8 on cfg4's first-seen decodes (profiles/r04_bsr_ab.json).
 // Coefficients: absolute routine addresses (BsrJob / BsrTblJob below).
 // ---------------------------------------------------------------------------
 #include "gf_routines.inc"
 
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
-constexpr int kBsrBatch = 4;          // inputs a wave loads at once
-constexpr uint32_t kBsrPhase = 8;     // inputs whose planes share LDS at a time (multi-wave form)
-// Wave priority of the plane-sharing table form's load stage (s_setprio while a
-// wave loads and transposes a phase's inputs, 0 for its routine calls): one
-// 64 MiB stripe of 30/70 0.070-0.072 -> 0.068-0.069 ms encode, 0.063-0.064 ->
-// 0.061 decode.  The other forms keep one priority: cfg4's first-seen decodes
-// (argument form) 0.430 -> 0.433-0.435 ms with it, 128/256 (combination
-// sharing) 0.121 -> 0.125 (160/256 0.123 -> 0.120); profiles/r05_bsr_prio_ab.json.
-constexpr int kBsrTblLoadPrio = 3;
+constexpr int kBsrBatch = 4;          // inputs a wave loads at once (combination-sharing form)
+typedef __attribute__((address_space(1))) void GlobalVoid;
+typedef __attribute__((address_space(3))) void LdsVoid;
 // Inputs per phase of the combination-sharing form (7.5 KiB each): one per wave,
 // so the 16 / nw workgroups a CU holds at 4 waves per SIMD take 120 KiB.
 __host__ __device__ constexpr uint32_t bsr_cmb_phase(uint32_t nw) { return nw; }
+// Inputs per phase of the plane-sharing form, whose LDS holds two phases: the
+// 16 / nw workgroups a CU holds at 4 waves per SIMD keep within its 160 KiB.
+__host__ __device__ constexpr uint32_t bsr_db_phase(uint32_t nw) { return nw <= 2 ? 2u : nw <= 4 ? 4u : 8u; }
 constexpr int kBsrMaxOut = 4 * kBsrMaxRows;  // rows of the kernel-argument form (4 tiles)
 constexpr int kBsrArgAddrs = 432;     // routine addresses the kernel-argument form holds
 
@@ -1248,8 +1246,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
-    const uint32_t kp = CMB ? bsr_cmb_phase(nw) : kBsrPhase;
-    constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
+    constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // (CMB) inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
     // block pointers and routine addresses: kernel arguments (BsrJob) or the
     // device-side table (BsrTblJob); the walk's "stripes" are (row group,
     // stripe) pairs, group-major
@@ -1285,54 +1282,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
         const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
         uint32_t acc[RT][8];  // no zeroing: the wave's first input calls "set" routines (kBsrSetBase)
-        for (uint32_t ph = 0; ph < k; ph += kp) {
-            const uint32_t kn = k - ph < kp ? k - ph : kp;
-            // inputs -> bit-planes -> LDS, inputs wave, wave + nw, ... in batches
-            if constexpr (TBL && !CMB) __builtin_amdgcn_s_setprio(kBsrTblLoadPrio);
-            for (uint32_t j0 = wave; j0 < kn; j0 += kBat * nw) {
-                u32x4 x[kBat][2];
-#pragma unroll
-                for (int q = 0; q < kBat; ++q) {
-                    const uint32_t j = j0 + q * nw;
-                    if (j < kn) {  // wave-uniform
-                        const uint8_t* ip = in_ptr(ph + j) + ib;
-                        x[q][0] = load16(ip);
-                        x[q][1] = load16(ip + 1024);
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < kBat; ++q) {
-                    const uint32_t j = j0 + q * nw;
-                    if (j < kn) {
-                        uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
-                                         x[q][1].x, x[q][1].y, x[q][1].z, x[q][1].w};
-                        transpose8(v);
-                        u32x4* b = bsr_planes + j * kIn;
-                        if constexpr (CMB) {  // every wave of the workgroup reads them: built once here
-                            uint32_t q[30];
-                            bsr_combos(v, q);
-#pragma unroll
-                            for (int g = 0; g < 7; ++g) b[g * 64 + lane] = u32x4{q[4 * g], q[4 * g + 1], q[4 * g + 2], q[4 * g + 3]};
-                            reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q[28], q[29]};
-                        } else {
-                            b[lane] = u32x4{v[0], v[1], v[2], v[3]};
-                            b[64u + lane] = u32x4{v[4], v[5], v[6], v[7]};
-                        }
-                    }
-                }
-            }
-            if constexpr (TBL && !CMB) __builtin_amdgcn_s_setprio(0);
-            __syncthreads();
-            // the phase's inputs in pairs with fixed address registers (A: even,
-            // B: odd): after input j's calls its set is reloaded (scalar loads,
-            // unconditional: clamped to the phase's last input) with input j + 2's
-            // addresses, which have all of input j + 1 to arrive (one wait drains
-            // LDS and scalar loads alike)
+        // the calls of one phase's kn inputs (ph, ph + 1, ...), planes or
+        // combinations at LDS offset o (u32x4): in pairs with fixed address
+        // registers (A: even, B: odd): after input j's calls its set is
+        // reloaded (scalar loads, unconditional: clamped to the phase's last
+        // input) with input j + 2's addresses, which have all of input j + 1 to
+        // arrive (one wait drains LDS and scalar loads alike)
+        auto calls = [&](uint32_t ph, uint32_t kn, uint32_t o) {
             uint64_t ada[RT], adb[RT];
             bsr_addrs<RT>(ada, ca, ph);
             bsr_addrs<RT>(adb, ca, ph + (kn > 1 ? 1 : 0));
             auto step = [&](uint32_t j, uint64_t (&ad)[RT]) {
-                const u32x4* b = bsr_planes + j * kIn;
+                const u32x4* b = bsr_planes + o + j * kIn;
                 if constexpr (CMB) {
                     uint32_t q[30];
 #pragma unroll
@@ -1360,7 +1321,88 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
                 step(j + 1, adb);
             }
             if (j < kn) step(j, ada);
-            __syncthreads();  // every wave has read the planes before they are overwritten
+        };
+        if constexpr (!CMB) {
+            // Planes: double-buffered phases of kq inputs.  A phase's inputs go
+            // straight into LDS (LDS-DMA, global_load_lds: no registers in
+            // flight) while the waves run the previous phase's calls, and are
+            // then transposed in place -- lane l's 16 + 16 bytes land in the
+            // slots its planes go to (b[l], b[64 + l]).  One barrier per phase.
+            const uint32_t kq = bsr_db_phase(nw);
+            auto dma = [&](uint32_t ph, uint32_t kn, uint32_t o) {
+                for (uint32_t j = wave; j < kn; j += nw) {
+                    const uint8_t* ip = in_ptr(ph + j) + ib;
+                    u32x4* b = bsr_planes + o + j * kIn;
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip), (LdsVoid*)(b), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip + 1024), (LdsVoid*)(b + 64), 16, 0, 0);
+                }
+            };
+            auto xpose = [&](uint32_t kn, uint32_t o) {
+                // hipcc does not order these LDS reads after the LDS-DMA writes
+                // (no vmcnt wait of its own here): wait for them explicitly
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (uint32_t j = wave; j < kn; j += nw) {
+                    u32x4* b = bsr_planes + o + j * kIn;
+                    const u32x4 x0 = b[lane], x1 = b[64u + lane];
+                    uint32_t v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                    transpose8(v);
+                    b[lane] = u32x4{v[0], v[1], v[2], v[3]};
+                    b[64u + lane] = u32x4{v[4], v[5], v[6], v[7]};
+                }
+            };
+            uint32_t kn = k < kq ? k : kq, o = 0;
+            dma(0, kn, 0);
+            xpose(kn, 0);
+            __syncthreads();
+            for (uint32_t ph = 0; ph < k; ph += kq) {
+                const uint32_t nx = ph + kq, knx = nx < k ? (k - nx < kq ? k - nx : kq) : 0u;
+                const uint32_t ox = o ^ (kq * kIn);  // the other half
+                if (knx) dma(nx, knx, ox);
+                calls(ph, kn, o);
+                if (knx) xpose(knx, ox);
+                __syncthreads();  // phase ph's planes read, phase nx's written
+                kn = knx;
+                o = ox;
+            }
+        } else {
+            // Combinations: phases of kp inputs, loaded through registers in
+            // batches, each input's 30 combinations built once and written to LDS
+            // for every wave; two barriers per phase
+            const uint32_t kp = bsr_cmb_phase(nw);
+            for (uint32_t ph = 0; ph < k; ph += kp) {
+                const uint32_t kn = k - ph < kp ? k - ph : kp;
+                for (uint32_t j0 = wave; j0 < kn; j0 += kBat * nw) {
+                    u32x4 x[kBat][2];
+#pragma unroll
+                    for (int q = 0; q < kBat; ++q) {
+                        const uint32_t j = j0 + q * nw;
+                        if (j < kn) {  // wave-uniform
+                            const uint8_t* ip = in_ptr(ph + j) + ib;
+                            x[q][0] = load16(ip);
+                            x[q][1] = load16(ip + 1024);
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < kBat; ++q) {
+                        const uint32_t j = j0 + q * nw;
+                        if (j < kn) {
+                            uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
+                                             x[q][1].x, x[q][1].y, x[q][1].z, x[q][1].w};
+                            transpose8(v);
+                            u32x4* b = bsr_planes + j * kIn;
+                            uint32_t q30[30];
+                            bsr_combos(v, q30);
+#pragma unroll
+                            for (int g = 0; g < 7; ++g)
+                                b[g * 64 + lane] = u32x4{q30[4 * g], q30[4 * g + 1], q30[4 * g + 2], q30[4 * g + 3]};
+                            reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q30[28], q30[29]};
+                        }
+                    }
+                }
+                __syncthreads();
+                calls(ph, kn, 0);
+                __syncthreads();  // every wave has read the combinations before they are overwritten
+            }
         }
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
@@ -2112,6 +2154,14 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 // 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json).
 bool bsr_cmb(uint32_t nw) { return nw >= 8; }
 
+// LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations,
+// or two of planes (one when a single phase holds all k).
+size_t bsr_lds_bytes(uint32_t k, uint32_t nw, bool cmb) {
+    const uint32_t ph = cmb ? bsr_cmb_phase(nw) : bsr_db_phase(nw);
+    if (cmb) return size_t(k < ph ? k : ph) * bsr_in_bytes<true>();
+    return size_t(k <= ph ? k : 2 * ph) * bsr_in_bytes<false>();
+}
+
 // nw = ceil(r / 10) waves, one per row tile of <= RT = ceil(r / nw) rows.
 struct BsrVariant {
     const void* fn = nullptr;
@@ -2480,9 +2530,8 @@ hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t b
     job.gs_c = static_cast<uint32_t>(grid % cps);
     job.addr = t.dev;
     const bool cmb = bsr_cmb(nw);
-    const uint32_t ph = cmb ? bsr_cmb_phase(nw) : kBsrPhase, kp = k < ph ? k : ph;
-    if ((e = launch_job(cmb ? g_bsr_tbl[rt].fn_cmb : g_bsr_tbl[rt].fn, grid, 64 * nw,
-                        size_t(kp) * (cmb ? bsr_in_bytes<true>() : bsr_in_bytes<false>()), stream, job)) != hipSuccess)
+    if ((e = launch_job(cmb ? g_bsr_tbl[rt].fn_cmb : g_bsr_tbl[rt].fn, grid, 64 * nw, bsr_lds_bytes(k, nw, cmb), stream,
+                        job)) != hipSuccess)
         return e;
     t_last_kernel = cmb ? g_bsr_tbl[rt].name_cmb : g_bsr_tbl[rt].name;
     return bsr_table_done(t, stream);
@@ -2534,10 +2583,9 @@ hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
         return launch_job(g_bsr_var[rt].fn_solo, grid, 64, 0, stream, job);
     }
     const bool cmb = bsr_cmb(nw);
-    const uint32_t ph = cmb ? bsr_cmb_phase(nw) : kBsrPhase, kp = k < ph ? k : ph;
     t_last_kernel = cmb ? g_bsr_var[rt].name_cmb : g_bsr_var[rt].name;
-    return launch_job(cmb ? g_bsr_var[rt].fn_cmb : g_bsr_var[rt].fn, grid, 64 * nw,
-                      size_t(kp) * (cmb ? bsr_in_bytes<true>() : bsr_in_bytes<false>()), stream, job);
+    return launch_job(cmb ? g_bsr_var[rt].fn_cmb : g_bsr_var[rt].fn, grid, 64 * nw, bsr_lds_bytes(k, nw, cmb), stream,
+                      job);
 }
 
 }  // namespace
