@@ -737,12 +737,14 @@ std::atomic<int> g_mode{-1};
 
 // Options of a kernel for an r x k matrix: the configured ones, with the
 // planes shared through LDS only while all k inputs' planes fit (2 KiB each),
-// and in phases of 8 inputs where all k at once would cap the residency below
-// what the kernel's registers allow (~3 waves per SIMD, i.e. 12 / tiles
-// workgroups per CU): the r = 20 decode of K=20/M=60 (2 tiles, 40 KiB: 2 waves
-// per SIMD) 0.672-0.694 -> 0.686-0.713 of HBM; its r = 40 encode (4 tiles,
-// register-bound either way) loses 0.678-0.691 -> 0.665 with phases, so keeps
-// all inputs (profiles/r05_jit_phase_ab.json).
+// and, where all k at once would cap the residency below what the kernel's
+// registers allow (~3 waves per SIMD, i.e. 12 / tiles workgroups per CU), in
+// double-buffered LDS-DMA phases of 4 inputs: the r = 20 decode of K=20/M=60
+// (2 tiles) 0.394 ms with register-loaded phases of 8 -> 0.377-0.382 (0.713 of
+// HBM; phases of 2: 0.446).  Its r = 40 encode (4 tiles, register-bound)
+// keeps one register-loaded phase of all 20 inputs: phases of 8 lost 0.678-0.691
+// -> 0.665 of HBM, phases of 4 by DMA 0.600 -> 0.649 ms and one DMA phase
+// 0.600 -> 0.615 (profiles/r05_jit_phase_ab.json, r05_lds_dma_ab.json).
 BsOptions options_for(unsigned k, unsigned r) {
     BsOptions o;
     if (k > 32) o.share = false;
