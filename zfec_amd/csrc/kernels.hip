@@ -1138,7 +1138,6 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 #include "gf_routines.inc"
 
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
-constexpr int kBsrBatch = 4;          // inputs a wave loads at once (combination-sharing form)
 typedef __attribute__((address_space(1))) void GlobalVoid;
 typedef __attribute__((address_space(3))) void LdsVoid;
 // Inputs per phase of the combination-sharing form (7.5 KiB each): one per wave,
@@ -1246,7 +1245,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nw = blockDim.x >> 6;
     const uint32_t k = job.k, r = job.r;
-    constexpr int kBat = RT >= 9 ? 2 : kBsrBatch;  // (CMB) inputs a wave loads at once (fewer past 8 rows: 4 waves per SIMD)
     // block pointers and routine addresses: kernel arguments (BsrJob) or the
     // device-side table (BsrTblJob); the walk's "stripes" are (row group,
     // stripe) pairs, group-major
@@ -1365,43 +1363,50 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
                 o = ox;
             }
         } else {
-            // Combinations: phases of kp inputs, loaded through registers in
-            // batches, each input's 30 combinations built once and written to LDS
-            // for every wave; two barriers per phase
-            const uint32_t kp = bsr_cmb_phase(nw);
-            for (uint32_t ph = 0; ph < k; ph += kp) {
-                const uint32_t kn = k - ph < kp ? k - ph : kp;
-                for (uint32_t j0 = wave; j0 < kn; j0 += kBat * nw) {
-                    u32x4 x[kBat][2];
-#pragma unroll
-                    for (int q = 0; q < kBat; ++q) {
-                        const uint32_t j = j0 + q * nw;
-                        if (j < kn) {  // wave-uniform
-                            const uint8_t* ip = in_ptr(ph + j) + ib;
-                            x[q][0] = load16(ip);
-                            x[q][1] = load16(ip + 1024);
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < kBat; ++q) {
-                        const uint32_t j = j0 + q * nw;
-                        if (j < kn) {
-                            uint32_t v[8] = {x[q][0].x, x[q][0].y, x[q][0].z, x[q][0].w,
-                                             x[q][1].x, x[q][1].y, x[q][1].z, x[q][1].w};
-                            transpose8(v);
-                            u32x4* b = bsr_planes + j * kIn;
-                            uint32_t q30[30];
-                            bsr_combos(v, q30);
-#pragma unroll
-                            for (int g = 0; g < 7; ++g)
-                                b[g * 64 + lane] = u32x4{q30[4 * g], q30[4 * g + 1], q30[4 * g + 2], q30[4 * g + 3]};
-                            reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q30[28], q30[29]};
-                        }
-                    }
+            // Combinations: phases of kp = nw inputs, one per wave.  A phase's
+            // inputs go into a raw staging area (LDS-DMA) while the waves walk
+            // the previous phase; after the barrier that ends it, each wave
+            // transposes its own input, builds its 30 combinations and writes
+            // them for every wave.
+            const uint32_t kp = bsr_cmb_phase(nw), oraw = (k < kp ? k : kp) * kIn;  // staging after the combinations
+            auto dma = [&](uint32_t ph, uint32_t kn) {
+                for (uint32_t j = wave; j < kn; j += nw) {
+                    const uint8_t* ip = in_ptr(ph + j) + ib;
+                    u32x4* b = bsr_planes + oraw + j * 128u;
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip), (LdsVoid*)(b), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip + 1024), (LdsVoid*)(b + 64), 16, 0, 0);
                 }
-                __syncthreads();
+            };
+            auto build = [&](uint32_t kn) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as in the planes form)
+                for (uint32_t j = wave; j < kn; j += nw) {
+                    const u32x4* r = bsr_planes + oraw + j * 128u;
+                    const u32x4 x0 = r[lane], x1 = r[64u + lane];
+                    uint32_t v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                    transpose8(v);
+                    uint32_t q30[30];
+                    bsr_combos(v, q30);
+                    u32x4* b = bsr_planes + j * kIn;
+#pragma unroll
+                    for (int g = 0; g < 7; ++g)
+                        b[g * 64 + lane] = u32x4{q30[4 * g], q30[4 * g + 1], q30[4 * g + 2], q30[4 * g + 3]};
+                    reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q30[28], q30[29]};
+                }
+            };
+            uint32_t kn = k < kp ? k : kp;
+            dma(0, kn);
+            build(kn);
+            __syncthreads();
+            for (uint32_t ph = 0; ph < k; ph += kp) {
+                const uint32_t nx = ph + kp, knx = nx < k ? (k - nx < kp ? k - nx : kp) : 0u;
+                if (knx) dma(nx, knx);  // each wave's staging slot: read by its own build() before the barrier
                 calls(ph, kn, 0);
                 __syncthreads();  // every wave has read the combinations before they are overwritten
+                if (knx) {
+                    build(knx);
+                    __syncthreads();
+                }
+                kn = knx;
             }
         }
 #pragma unroll
@@ -2154,11 +2159,12 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 // 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json).
 bool bsr_cmb(uint32_t nw) { return nw >= 8; }
 
-// LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations,
-// or two of planes (one when a single phase holds all k).
+// LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations
+// and its raw staging, or two phases of planes (one when a single phase holds
+// all k).
 size_t bsr_lds_bytes(uint32_t k, uint32_t nw, bool cmb) {
     const uint32_t ph = cmb ? bsr_cmb_phase(nw) : bsr_db_phase(nw);
-    if (cmb) return size_t(k < ph ? k : ph) * bsr_in_bytes<true>();
+    if (cmb) return size_t(k < ph ? k : ph) * (bsr_in_bytes<true>() + bsr_in_bytes<false>());  // + raw staging
     return size_t(k <= ph ? k : 2 * ph) * bsr_in_bytes<false>();
 }
 
