@@ -59,9 +59,11 @@ def is_bsr(name, r, units=0):
     return name.startswith(want) and name[len(want)] in ">,"
 
 
-# (k, m): r = m - k = 1..10 (one wave, RT = r), 13 / 20 (two waves), 25 (three), 31 / 40 (four)
+# (k, m): r = m - k = 1..10 (one wave, RT = r), 13 / 20 (two waves), 25 (three), 31 / 40 (four);
+# odd k on the double-buffered LDS phases (a short last phase: 9 and 15 inputs in phases of 2 on
+# two waves, 13 in phases of 4 on four)
 SHAPES = [(30, 31), (12, 14), (10, 13), (7, 11), (6, 11), (10, 16), (5, 12), (20, 28), (3, 12), (32, 42),
-          (20, 33), (12, 32), (16, 41), (2, 33), (20, 60), (32, 72)]
+          (20, 33), (12, 32), (16, 41), (2, 33), (20, 60), (32, 72), (9, 20), (15, 27), (13, 30)]
 
 
 @pytest.mark.parametrize("k,m", SHAPES)
