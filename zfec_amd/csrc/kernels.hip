@@ -1140,8 +1140,9 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
 typedef __attribute__((address_space(1))) void GlobalVoid;
 typedef __attribute__((address_space(3))) void LdsVoid;
-// Inputs per phase of the combination-sharing form (7.5 KiB each): one per wave,
-// so the 16 / nw workgroups a CU holds at 4 waves per SIMD take 120 KiB.
+// Inputs per phase of the combination-sharing form (7.5 KiB of combinations +
+// 2 KiB of raw staging each): one per wave, so the 16 / nw workgroups a CU
+// holds at 4 waves per SIMD take 152 KiB.
 __host__ __device__ constexpr uint32_t bsr_cmb_phase(uint32_t nw) { return nw; }
 // Inputs per phase of the plane-sharing form, whose LDS holds two phases: the
 // 16 / nw workgroups a CU holds at 4 waves per SIMD keep within its 160 KiB.
@@ -2156,7 +2157,8 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 // planes (the 22 multi-plane combinations rebuilt by every wave): with 8 waves,
 // where rebuilding is 8x the work (128/256 0.130 -> 0.122 ms per 64 MiB stripe);
 // with 2 or 4 the short phases cost more than the XORs saved (cfg4's first-seen
-// 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json).
+// 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json;
+// on DMA-staged phases 0.419 -> 0.428 and 0.065 -> 0.067, r05_lds_dma_ab.json).
 bool bsr_cmb(uint32_t nw) { return nw >= 8; }
 
 // LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations
