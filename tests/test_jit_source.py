@@ -1,0 +1,71 @@
+"""CPU checks of the generated source of the bit-sliced kernels' double-buffered
+LDS-DMA phases (zfec_amd/csrc/bitslice.cpp, the shared-input form of the
+zfec/fec.c:487-505 / :527-557 apply): every tile branch meets the same
+barriers, every LDS-DMA target and plane read stays inside the declared LDS,
+each wave waits for one DMA'd phase per phase of the matrix, and a kernel whose
+inputs all fit keeps its single register-loaded phase.  No GPU: the kernels are
+generated and compiled for gfx950 by hipRTC here."""
+import re
+
+import pytest
+
+from zfec_amd import capi
+
+
+def place(nums, k):
+    """slot order with primary i at slot i (zfec/_fecmodule.c:482-493)."""
+    slots = [None] * k
+    sec = iter([n for n in nums if n >= k])
+    for n in nums:
+        if n < k:
+            slots[n] = n
+    return [s if s is not None else next(sec) for s in slots]
+
+
+def generated(tmp_path, monkeypatch, k, m, decode):
+    monkeypatch.setenv("ZFEC_HIP_JIT_CACHE", str(tmp_path / "cache"))
+    dump = tmp_path / "dump"
+    dump.mkdir()
+    monkeypatch.setenv("ZFEC_HIP_JIT_DUMP", str(dump))
+    code = capi.Code(k, m)
+    if decode:
+        code.jit_prepare_decode(place(list(range(m - k, m)), k))
+    else:
+        code.jit_prepare_encode(list(range(k, m)))
+    files = list(dump.glob("zfec_hip_bitslice_k%d_r*.hip" % k))
+    assert len(files) == 1, files
+    return files[0].read_text()
+
+
+# decodes from the last k blocks: r = 18 / 27 / 20 rows on 2 / 3 / 2 tiles, phases of 4 with a
+# short last one for k = 17 and 23
+@pytest.mark.parametrize("k,m", [(17, 35), (23, 50), (20, 60)])
+def test_dma_phase_structure(tmp_path, monkeypatch, k, m):
+    src = generated(tmp_path, monkeypatch, k, m, decode=True)
+    size = int(re.search(r"__shared__ u32x4 sh\[(\d+)\]", src).group(1))
+    assert size == 2 * 4 * 128, size  # two phases of 4 inputs, 128 u32x4 each
+    # every DMA target and every plane access inside the declared LDS
+    for off in re.findall(r"sh \+ (\d+)u", src):
+        assert int(off) + 64 <= size, off
+    for off in re.findall(r"sh\[(\d+)u \+ lane\]", src):
+        assert int(off) + 64 <= size, off
+    body = src[src.index("while (s < a.nstripes)"):]
+    branches = re.split(r"if \(tile == \d+u\) \{", body)[1:]
+    nphases = -(-k // 4)
+    bars = [b.count("__syncthreads()") for b in branches]
+    bars[-1] -= 1  # the unit's closing barrier follows the last branch
+    assert len(set(bars)) == 1 and bars[0] == nphases, bars
+    for b in branches:
+        # one wait per phase, each after the DMA it waits for
+        assert b.count("dma_wait()") == nphases
+        assert b.index("dma16(") < b.index("dma_wait()")
+        assert b.count("dma16(") >= 2 * (nphases - 1)
+
+
+def test_single_phase_kernel_keeps_register_loads(tmp_path, monkeypatch):
+    """K=20/M=60's r = 40 encode (4 tiles: all 20 inputs fit) loads through
+    registers in one phase; the DMA phases lost 2-8 % there
+    (profiles/r05_lds_dma_ab.json)."""
+    src = generated(tmp_path, monkeypatch, 20, 60, decode=False)
+    assert "dma16(ka->" not in src and "dma_wait();" not in src
+    assert int(re.search(r"__shared__ u32x4 sh\[(\d+)\]", src).group(1)) == 20 * 128
