@@ -940,9 +940,30 @@ def run_first_seen(npat=FIRST_SEEN_PATTERNS):
     out = torch.empty((ns, k, ld), dtype=torch.uint8, device="cuda")
     code = capi.Code(k, m)
     stream = torch.cuda.current_stream()
-    code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, list(range(k, m)), sz, ns,
-                      stream=stream.cuda_stream)
-    LEGS.add("first-seen setup", capi.last_kernel_name())
+    nums = list(range(k, m))
+
+    def enc_once(order, leg):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, order, sz, ns,
+                          stream=stream.cuda_stream, flags=ROW_PADDING_FLAGS)
+        b.record(stream)
+        kern = capi.last_kernel_name()
+        LEGS.add(leg, kern)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b), kern
+
+    # the process's first launch of this code's encode matrix (host work of the
+    # launch -- the routine table's address probe, the address-table upload --
+    # inside the events)
+    t_first, k_first = enc_once(nums, "first-launch encode setup")
+    ref = par[::97, :, :sz].clone()  # a sample of stripes: the parity every later encode is checked against
+
+    def enc_check(order):
+        got = par[::97, :, :sz]
+        for j, b in enumerate(order):
+            assert torch.equal(got[:, j], ref[:, b - k]), "first-launch encode != the code's parity"
+
     jit_slots = list(range(m - k, m))
     code.jit_prepare_decode(jit_slots)  # loads (or compiles) the compiled kernel of this one pattern
     rng = np.random.default_rng(5005)
@@ -988,6 +1009,44 @@ def run_first_seen(npat=FIRST_SEEN_PATTERNS):
             e["valu_roofline"] = valu_roofline("first_seen", kern[0], mean)
         res[tag] = e
     res["first_seen_vs_jit"] = round(res["jit"]["ms_mean"] / res["first_seen"]["ms_mean"], 4)
+    # first_launch_encode: encodes of all 40 parity rows in `npat` row orders the
+    # process has never launched (each order a new matrix, so each launch is a
+    # first launch: no compiled kernel exists for it), against the compiled
+    # kernel of the natural order (fec_jit_prepare_encode)
+    hbm_e = lambda ms: (k + r) * sz * ns / (ms * 1e-3) / 1e9
+    fl = {"shape": "K=20/M=60, %d x 1 MiB stripes, encode of all %d parity rows" % (ns, r),
+          "algorithmic_bytes_per_launch": (k + r) * sz * ns,
+          "process_first_launch": {"kernel": k_first, "ms_incl_host": round(t_first, 4),
+                                   "note": "the process's first launch of the code (natural row order), between "
+                                           "events that also hold its one-time host work (routine-table probe, "
+                                           "address-table upload)"}}
+    orders = [nums[i:] + nums[:i] for i in range(1, npat + 2)]
+    enc_once(orders[0], "first-launch encode (untimed)")
+    enc_check(orders[0])
+    rows = []
+    for o in orders[1:]:
+        rows.append(enc_once(o, "first-launch encode"))
+        enc_check(o)
+    code.jit_prepare_encode(nums)
+    enc_once(nums, "first-launch jit encode (untimed)")
+    jrows = [enc_once(nums, "first-launch jit encode") for _ in range(npat)]
+    enc_check(nums)
+    for tag, rr in (("first_launch", rows), ("jit", jrows)):
+        ms = [x for x, _ in rr]
+        kern = sorted(set(n for _, n in rr))
+        mean = float(np.mean(ms))
+        e = {"kernel": kern[0] if len(kern) == 1 else kern, "ms_mean": round(mean, 4),
+             "ms_min": round(float(np.min(ms)), 4), "ms_max": round(float(np.max(ms)), 4),
+             "hbm_GBps": round(hbm_e(mean), 1), "frac_of_peak": round(hbm_e(mean) / HBM_PEAK_GBPS, 4),
+             "input_GBps": round(k * sz * ns / (mean * 1e-3) / 1e9, 1)}
+        if len(kern) == 1:
+            e["valu_roofline"] = valu_roofline("first_launch", kern[0], mean)
+        fl[tag] = e
+    fl["first_launch_vs_jit"] = round(fl["jit"]["ms_mean"] / fl["first_launch"]["ms_mean"], 4)
+    fl["timing"] = ("one encode launch per row order between HIP events, the orders rotations of the 40 parity "
+                    "numbers the process has not launched (each a matrix with no compiled kernel), JIT mode as "
+                    "shipped; one untimed launch of each kind first; parity checked on a sample of stripes")
+    res["first_launch_encode"] = fl
     res["timing"] = ("one decode launch per pattern between HIP events (staging copies outside), JIT mode as "
                      "shipped (auto): a first-seen matrix has no compiled kernel; one untimed launch of each kind "
                      "first")
@@ -1134,6 +1193,7 @@ def main():
         out["batched_1MiB"] = run_batched_1mib(20)
     if rank == 0 and not args.no_first_seen and args.workload == "cfg2":
         out["first_seen_decode"] = run_first_seen()
+        out["first_launch_encode"] = out["first_seen_decode"].pop("first_launch_encode")
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             csz = min(sz, -(-(64 << 20) // k))  # sample stripes of at most 64 MiB (same K/M)

@@ -2,13 +2,17 @@
 routines matapply_bsr calls (one per coefficient):
 
 - the file is what tools/gen_gf_routines.py writes (no hand edits, no stale copy);
-- every routine, executed by a small interpreter of its v_bitop3_b32 lines on
-  bit-planes of random bytes -- after the combination XORs that bsr_input emits
-  -- adds exactly c * x (the oracle's gf_mul, zfec/fec.c:58-86 via
-  oracle/fec_oracle.c) to the accumulator row;
+- every routine, executed by a small interpreter of its lines (v_bitop3_b32
+  XOR3, VOP2 v_xor_b32, VOP1 v_mov_b32) on bit-planes of random bytes -- after
+  the combination XORs that bsr_input emits -- adds exactly c * x (the
+  oracle's gf_mul, zfec/fec.c:58-86 via oracle/fec_oracle.c) to the
+  accumulator row, reading the row only where the index mode of its caller
+  indexes it (SRC0 of the accumulate routines; the set twins' callers index
+  the destination only);
 - the "set" twins (256 + c) write c * x over the row;
 - every routine fits its 72-byte slot (the .org directives would fail the
-  build otherwise; this names the routine)."""
+  build otherwise; this names the routine);
+- the round-5 form (--form legacy) passes the same interpreter."""
 
 import os
 import re
@@ -30,8 +34,8 @@ def test_generated_file_is_current():
     assert r.returncode == 0, "gf_routines.inc differs from tools/gen_gf_routines.py output"
 
 
-def _parse():
-    text = open(INC).read()
+def _parse(text=None):
+    text = text if text is not None else open(INC).read()
     body = text[text.index('"zfec_gf_routines:\\n"'):text.index('"zfec_gf_routines_end:')]
     routines = {}
     for m in re.finditer(r'"\.org zfec_gf_routines \+ (\d+)\\n"\s*\n\s*"([^"]*)"', body):
@@ -46,22 +50,39 @@ def _planes(x):
     return [int(sum(((int(x[t]) >> b) & 1) << t for t in range(32))) for b in range(8)]
 
 
-def test_every_routine_multiplies():
-    """Routines 0-255 add c * x to the row; 256-511 (the "set" twins a wave's
-    first input calls) write c * x over whatever the row held."""
-    routines, xors = _parse()
+_OPS = [
+    # (regex, kind): XOR3 of the accumulator (or, 0x66, of nothing) and two combinations
+    (re.compile(r"v_bitop3_b32 v(\d+), v(\d+), (v\d+|0), (v\d+|0) bitop3:(0x96|0x66)"), "bitop3"),
+    (re.compile(r"v_xor_b32 v(\d+), (v\d+), (v\d+)"), "xor"),
+    (re.compile(r"v_mov_b32 v(\d+), (v\d+|0)"), "mov"),
+]
+
+
+def _bytes(line):
+    return 8 if line.startswith("v_bitop3") else 4
+
+
+def _check_routines(routines, xors, form):
     assert len(routines) == 512 and len(xors) == 22
     rng = np.random.default_rng(72)
     mul = np.array([[oracle.gf_mul(a, b) for b in range(256)] for a in range(256)], dtype=np.uint8)
-    op = re.compile(r"v_bitop3_b32 v(\d+), v(\d+), (v\d+|0), (v\d+|0) bitop3:(0x96|0x66)")
     for slot in range(512):
         c, first = slot % 256, slot >= 256
         lines = routines[72 * slot]
         assert lines[-2] == "s_setpc_b64 s[30:31]" and lines[-1] == "", (slot, lines[-2:])
         body = lines[:-2]
-        assert 8 * len(body) + 4 <= 72, slot
+        assert sum(_bytes(ln) for ln in body) + 4 <= 72, slot
+        parsed = []
+        for ln in body:
+            for rx, kind in _OPS:
+                m = rx.fullmatch(ln)
+                if m:
+                    parsed.append((kind, m.groups()))
+                    break
+            else:
+                raise AssertionError((slot, ln))
         if first:  # every plane written
-            assert sorted(int(op.fullmatch(ln).group(1)) for ln in body) == list(range(ACC, ACC + 8)), slot
+            assert sorted(int(g[0]) for _, g in parsed) == list(range(ACC, ACC + 8)), slot
         for trial in range(3):
             x = rng.integers(0, 256, size=32, dtype=np.uint8)
             acc0 = rng.integers(0, 256, size=32, dtype=np.uint8)
@@ -72,16 +93,51 @@ def test_every_routine_multiplies():
                 v[d] = v[a] ^ v[b]
             for b, pl in enumerate(_planes(acc0)):
                 v[ACC + b] = pl
-            for ln in body:
-                m = op.fullmatch(ln)
-                assert m, (slot, ln)
-                d, s0, s1, s2, tt = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4), m.group(5)
-                assert d == s0 and ACC <= d < ACC + 8, (slot, ln)
-                assert tt == ("0x66" if first else "0x96"), (slot, ln)
-                val = lambda s: 0 if s == "0" else v[int(s[1:])]
-                v[d] = (0 if first else v[s0]) ^ val(s1) ^ val(s2)
+            val = lambda s: 0 if s == "0" else v[int(s[1:])]
+            # the row (v38..v45, offset by the caller's index) is a source only where
+            # the caller's mode indexes it: SRC0 of the accumulate routines (legacy:
+            # of the set twins too, whose 0x66 ignores it); never a set twin's source
+            # in the vop2 form (its callers index the destination only)
+            for kind, g in parsed:
+                d = int(g[0])
+                assert ACC <= d < ACC + 8, (slot, kind, g)
+                if kind == "bitop3":
+                    s0, s1, s2, tt = int(g[1]), g[2], g[3], g[4]
+                    assert s0 == d, (slot, g)
+                    assert tt == ("0x66" if first else "0x96"), (slot, g)
+                    assert not (first and form == "vop2"), (slot, "set twins are VOP1/VOP2 in the vop2 form")
+                    v[d] = (0 if first else v[s0]) ^ val(s1) ^ val(s2)
+                elif kind == "xor":
+                    s0, s1 = g[1], g[2]
+                    assert form == "vop2", (slot, g)
+                    if first:  # sources: two combinations, none of them a row register
+                        assert all(not (ACC <= int(s[1:]) < ACC + 8) for s in (s0, s1)), (slot, g)
+                        v[d] = val(s0) ^ val(s1)
+                    else:  # src0 the (indexed) row, src1 an unindexed combination
+                        assert int(s0[1:]) == d and not (ACC <= int(s1[1:]) < ACC + 8), (slot, g)
+                        v[d] = v[d] ^ val(s1)
+                else:
+                    assert form == "vop2" and first, (slot, g)
+                    assert g[1] == "0" or not (ACC <= int(g[1][1:]) < ACC + 8), (slot, g)
+                    v[d] = val(g[1])
             want = _planes(mul[c][x] if first else acc0 ^ mul[c][x])
             assert [v[ACC + b] for b in range(8)] == want, (slot, trial)
+
+
+def test_every_routine_multiplies():
+    """Routines 0-255 add c * x to the row; 256-511 (the "set" twins a wave's
+    first input calls) write c * x over whatever the row held."""
+    routines, xors = _parse()
+    _check_routines(routines, xors, "vop2")
+
+
+def test_legacy_form_multiplies(tmp_path):
+    """The round-5 form kept for the A/B (tools/ab_build.sh `legacy`)."""
+    out = tmp_path / "legacy.inc"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_gf_routines.py"), "--form", "legacy", "--out",
+                    str(out)], check=True)
+    routines, xors = _parse(out.read_text())
+    _check_routines(routines, xors, "legacy")
 
 
 def test_every_call_statement_restores_m0():
@@ -90,10 +146,12 @@ def test_every_call_statement_restores_m0():
     each bsr_input<RT> statement must save M0 into an early-clobber SGPR before
     its first index-mode call and restore it after its last one."""
     text = open(INC).read()
-    bodies = re.findall(r"void bsr_input(?:_c)?<(\d+)>\(.*?asm volatile\((.*?)\);\n\}", text, re.S)
-    # bsr_input<1..10> (combinations built in the statement), bsr_input_c<1..10> (read from LDS)
-    assert [int(rt) for rt, _ in bodies] == list(range(1, 11)) * 2
-    for rt, body in bodies:
+    bodies = re.findall(r"void (bsr_input(?:_c)?(?:_first)?)<(\d+)>\(.*?asm volatile\((.*?)\);\n\}", text, re.S)
+    # bsr_input<1..10> (combinations built in the statement), bsr_input_first (the set
+    # twins), bsr_input_c<1..10> (combinations as inputs), bsr_input_c_first
+    assert [(fam, int(rt)) for fam, rt, _ in bodies] == [
+        (fam, rt) for fam in ("bsr_input", "bsr_input_first", "bsr_input_c", "bsr_input_c_first") for rt in range(1, 11)]
+    for fam, rt, body in bodies:
         ins = [s for s in re.findall(r'"([^"]*)"', body.split("\n        :")[0])]
         ins = [ln.replace("\\n\\t", "") for ln in ins]
         save = [i for i, ln in enumerate(ins) if re.fullmatch(r"s_mov_b32 %(\d+), m0", ln)]
@@ -104,6 +162,10 @@ def test_every_call_statement_restores_m0():
         calls = [i for i, ln in enumerate(ins) if ln.startswith("s_swappc_b64")]
         # index mode on once, moved to row rr (8 rr) before each later call, off after the last
         assert len(idx_on) == 1 and len(idx_off) == 1 and len(calls) == int(rt), rt
+        # the set twins run with only the destination indexed (their sources are
+        # combinations); the accumulate routines index SRC0 (the row) and DST
+        mode = "gpr_idx(DST)" if fam.endswith("_first") else "gpr_idx(SRC0,DST)"
+        assert ins[idx_on[0]] == "s_set_gpr_idx_on 0, " + mode, (fam, rt, ins[idx_on[0]])
         assert [ins[i] for i in idx_idx] == ["s_set_gpr_idx_idx %d" % (8 * rr) for rr in range(1, int(rt))], rt
         assert idx_on[0] < calls[0] and calls[-1] < idx_off[0], rt
         assert all(calls[rr - 1] < idx_idx[rr - 1] < calls[rr] for rr in range(1, int(rt))), rt

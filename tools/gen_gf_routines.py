@@ -39,8 +39,20 @@ Register contract (fixed by the routines' encodings):
                 it last (s_nop 0 after the restore: an M0 write followed by an
                 LDS-DMA / s_movrel needs one wait state)
 
+Instruction forms (round 6).  On gfx950 a wave64 v_xor_b32 / v_mov_b32 issues
+in half the cycles of any VOP3 instruction (v_bitop3_b32, shifts: 57-66 against
+36-40 T lane-ops/s, profiles/r02_mb_valu.log), so a plane with one nibble
+empty is `v_xor_b32 acc, acc, x` (VOP2: in gpr_idx(SRC0,DST) mode src0 is the
+indexed accumulator, src1 the unindexed combination) and the "set" twins --
+which ignore the row's old value -- are `v_xor_b32 acc, L, H` / `v_mov_b32 acc,
+x`: their sources must not be indexed, so the first input's statement
+(bsr_input_first / bsr_input_c_first) runs them in gpr_idx(DST) mode.
+`--form legacy` writes round 5's routines (every plane a v_bitop3_b32, the set
+twins in SRC0,DST mode) for the A/B (tools/ab_bsr.sh).
+
     python tools/gen_gf_routines.py            # rewrite the .inc
     python tools/gen_gf_routines.py --check    # exit 1 if it is stale
+    python tools/gen_gf_routines.py --form legacy --out PATH
 """
 import os
 import sys
@@ -76,32 +88,104 @@ def masks(c):
     return out
 
 
-def routine(c, first=False):
-    """Routine c adds c*x to the accumulator row (acc_b ^= L ^ H, XOR3 = truth
-    table 0x96); with first=True it sets the row to c*x instead (acc_b = L ^ H,
-    truth table 0x66: the first operand, the row's old value, is ignored), so a
-    wave's first input needs no zeroed accumulators."""
+def routine(c, first=False, form="vop2"):
+    """Routine c adds c*x to the accumulator row (acc_b ^= L ^ H); with
+    first=True it sets the row to c*x instead (acc_b = L ^ H), so a wave's
+    first input needs no zeroed accumulators.  form "legacy": every plane a
+    v_bitop3_b32 (XOR3, truth table 0x96; the set twins 0x66, which ignores
+    the row's old value, in SRC0,DST index mode).  form "vop2": XOR3 only
+    where both nibbles are non-empty, VOP2 v_xor_b32 / VOP1 v_mov_b32 for the
+    rest; the set twins run in DST-only index mode."""
     lines = []
     for b, (ml, mh) in enumerate(masks(c)):
+        acc = ACC + b
         if not ml and not mh and not first:
             continue
-        s1 = "v%d" % reg(0, ml) if ml else "0"
-        s2 = "v%d" % reg(1, mh) if mh else "0"
-        lines.append("v_bitop3_b32 v%d, v%d, %s, %s bitop3:%s" % (ACC + b, ACC + b, s1, s2, "0x66" if first else "0x96"))
+        sl = "v%d" % reg(0, ml) if ml else None
+        sh = "v%d" % reg(1, mh) if mh else None
+        if form == "legacy":  # (trunc64: the vop2 instructions, cut below)
+            lines.append("v_bitop3_b32 v%d, v%d, %s, %s bitop3:%s" % (acc, acc, sl or "0", sh or "0",
+                                                                     "0x66" if first else "0x96"))
+        elif first:
+            if sl and sh:
+                lines.append("v_xor_b32 v%d, %s, %s" % (acc, sl, sh))
+            else:
+                lines.append("v_mov_b32 v%d, %s" % (acc, sl or sh or "0"))
+        elif sl and sh:
+            lines.append("v_bitop3_b32 v%d, v%d, %s, %s bitop3:0x96" % (acc, acc, sl, sh))
+        else:
+            lines.append("v_xor_b32 v%d, v%d, %s" % (acc, acc, sl or sh))
+    if form == "trunc64":  # timing experiment only (wrong results): every routine cut to 64 bytes
+        # (form "inline": the statements run one fixed routine's body in place of each call)
+        while routine_bytes(lines) + 4 > 64:
+            lines.pop()
     lines.append("s_setpc_b64 s[30:31]")
-    assert 8 * (len(lines) - 1) + 4 <= STRIDE
+    assert routine_bytes(lines) <= STRIDE
     return lines
 
 
-def render():
+def routine_bytes(lines):
+    """Encoded size: VOP3 (v_bitop3_b32) 8 bytes, VOP1/VOP2 and SOP1 4."""
+    return sum(8 if ln.startswith("v_bitop3") else 4 for ln in lines)
+
+
+def statement(o, rt, cmb, first, form):
+    """The asm statement of one input's calls for a wave of rt rows: cmb=False
+    builds the 22 multi-plane combinations from the planes (bsr_input), cmb=True
+    takes all 30 as inputs (bsr_input_c); first=True calls the set twins (the
+    wave's first input), in DST-only index mode in the vop2 form."""
+    mode = "gpr_idx(DST)" if first and form != "legacy" else "gpr_idx(SRC0,DST)"
+    o.append("    uint32_t keep;  // M0, saved and restored around the index-mode calls")
+    o.append("    asm volatile(")
+    o.append("        \"s_mov_b32 %%%d, m0\\n\\t\"" % (8 * rt))
+    if not cmb:
+        for side in (0, 1):
+            for m in MULTI:
+                top = 1 << (m.bit_length() - 1)
+                o.append("        \"v_xor_b32 v%d, v%d, v%d\\n\\t\"" % (reg(side, m), reg(side, m ^ top), reg(side, top)))
+    nout = 8 * rt
+    nin = 8 if not cmb else 30
+    for rr in range(rt):
+        if rr == 0:
+            o.append("        \"s_set_gpr_idx_on 0, %s\\n\\t\"" % mode)
+        else:
+            o.append("        \"s_set_gpr_idx_idx %d\\n\\t\"" % (8 * rr))
+        if form == "inline":  # timing experiment only (wrong results): a fixed routine's body, no call
+            c = next(c for c in range(255, 0, -1) if all(ml and mh for ml, mh in masks(c)))
+            for ln in routine(c, first=first, form="vop2")[:-1]:
+                o.append("        \"%s\\n\\t\"" % ln)
+            o.append("        \"s_nop 0 ; %%%d\\n\\t\"" % (nout + 1 + nin + rr))
+            continue
+        o.append("        \"s_swappc_b64 s[30:31], %%%d\\n\\t\"" % (nout + 1 + nin + rr))
+    o.append("        \"s_set_gpr_idx_off\\n\\t\"")
+    o.append("        \"s_mov_b32 m0, %%%d\\n\\t\"" % nout)
+    o.append("        \"s_nop 0\"")
+    cons = "=" if first else "+"  # the set twins write every row they are called for
+    outs = ['"%s{v%d}"(acc[%d][%d])' % (cons, ACC + 8 * rr + b, rr, b) for rr in range(rt) for b in range(8)]
+    outs.append('"=&s"(keep)')
+    if cmb:
+        ins = ['"{v%d}"(q[%d])' % (PL + d, d) for d in range(30)]
+    else:
+        ins = ['"{v%d}"(p[%d])' % (PL + b, b) for b in range(8)]
+    ins += ['"s"(addr[%d])' % rr for rr in range(rt)]
+    clob = [] if cmb else ['"v%d"' % v for v in range(CB, CB + 22)]
+    clob += ['"s30"', '"s31"', '"scc"']
+    o.append("        : " + ", ".join(outs))
+    o.append("        : " + ", ".join(ins))
+    o.append("        : " + ", ".join(clob) + ");")
+
+
+def render(form="vop2"):
+    stride = 64 if form == "trunc64" else STRIDE
     o = []
     o.append("// gf_routines.inc -- generated by tools/gen_gf_routines.py; do not edit.")
     o.append("// The multiply-by-constant routines of matapply_bsr and the per-row calls")
-    o.append("// into them (register contract in the generator's docstring).")
+    o.append("// into them (register contract and instruction forms in the generator's")
+    o.append("// docstring).  Form: %s." % form)
     o.append("#pragma once")
-    o.append("constexpr uint32_t kBsrStride = %d;   // bytes per routine" % STRIDE)
+    o.append("constexpr uint32_t kBsrStride = %d;   // bytes per routine" % stride)
     o.append("constexpr int kBsrMaxRows = %d;       // accumulator rows a wave can hold" % MAX_ROWS)
-    o.append("constexpr uint32_t kBsrSetBase = %d;  // byte offset of the \"set\" routines (256 + c)" % (STRIDE * 256))
+    o.append("constexpr uint32_t kBsrSetBase = %d;  // byte offset of the \"set\" routines (256 + c)" % (stride * 256))
     # clang drops file-scope asm from device compilations: the table is the body
     # of a device function nothing calls (kept by `used`; its label is a symbol
     # of the code object the kernels' calls resolve against)
@@ -110,9 +194,9 @@ def render():
     o.append("    \".p2align 6\\n\"")
     o.append("    \"zfec_gf_routines:\\n\"")
     for c in range(512):
-        o.append("    \".org zfec_gf_routines + %d\\n\"" % (STRIDE * c))
-        o.append("    \"" + "\\n".join(routine(c % 256, first=c >= 256)) + "\\n\"")
-    o.append("    \".org zfec_gf_routines + %d\\n\"" % (STRIDE * 512))
+        o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * c))
+        o.append("    \"" + "\\n".join(routine(c % 256, first=c >= 256, form=form)) + "\\n\"")
+    o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * 512))
     o.append("    \"zfec_gf_routines_end:\\n\");")
     o.append("}")
     o.append("")
@@ -122,79 +206,37 @@ def render():
     o.append("// written by the host).  Builds the 22 multi-plane combinations, then calls")
     o.append("// row rr's routine with the accumulator index at 8 * rr: index mode is set")
     o.append("// once and moved per row (s_set_gpr_idx_idx), so a row costs three scalar")
-    o.append("// instructions (index, call, return).")
-    o.append("template <int RT>")
-    o.append("__device__ __forceinline__ void bsr_input(uint32_t (&acc)[RT][8], const uint32_t (&p)[8],")
-    o.append("                                          const uint64_t (&addr)[RT]);")
-    for rt in range(1, MAX_ROWS + 1):
-        o.append("template <>")
-        o.append("__device__ __forceinline__ void bsr_input<%d>(uint32_t (&acc)[%d][8], const uint32_t (&p)[8]," % (rt, rt))
-        o.append("                                             const uint64_t (&addr)[%d]) {" % rt)
-        o.append("    uint32_t keep;  // M0, saved and restored around the index-mode calls")
-        o.append("    asm volatile(")
-        o.append("        \"s_mov_b32 %%%d, m0\\n\\t\"" % (8 * rt))
-        for side in (0, 1):
-            for m in MULTI:
-                top = 1 << (m.bit_length() - 1)
-                o.append("        \"v_xor_b32 v%d, v%d, v%d\\n\\t\"" % (reg(side, m), reg(side, m ^ top), reg(side, top)))
-        nout = 8 * rt
-        for rr in range(rt):
-            if rr == 0:
-                o.append("        \"s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\\n\\t\"")
-            else:
-                o.append("        \"s_set_gpr_idx_idx %d\\n\\t\"" % (8 * rr))
-            o.append("        \"s_swappc_b64 s[30:31], %%%d\\n\\t\"" % (nout + 1 + 8 + rr))
-        o.append("        \"s_set_gpr_idx_off\\n\\t\"")
-        o.append("        \"s_mov_b32 m0, %%%d\\n\\t\"" % nout)
-        o.append("        \"s_nop 0\"")
-        outs = ['"+{v%d}"(acc[%d][%d])' % (ACC + 8 * rr + b, rr, b) for rr in range(rt) for b in range(8)]
-        outs.append('"=&s"(keep)')
-        ins = ['"{v%d}"(p[%d])' % (PL + b, b) for b in range(8)] + ['"s"(addr[%d])' % rr for rr in range(rt)]
-        clob = ['"v%d"' % v for v in range(CB, CB + 22)] + ['"s30"', '"s31"', '"scc"']
-        o.append("        : " + ", ".join(outs))
-        o.append("        : " + ", ".join(ins))
-        o.append("        : " + ", ".join(clob) + ");")
-        o.append("}")
-    o.append("")
-    o.append("// bsr_input_c<RT>(acc, q, addr): the same with the input's 30 combinations (planes")
-    o.append("// and the 22 multi-plane XORs, in register order v%d..v%d) built once per workgroup" % (PL, CB + 21))
-    o.append("// and read from LDS by every wave (matapply_bsr's combination-sharing form).")
-    o.append("template <int RT>")
-    o.append("__device__ __forceinline__ void bsr_input_c(uint32_t (&acc)[RT][8], const uint32_t (&q)[30],")
-    o.append("                                            const uint64_t (&addr)[RT]);")
-    for rt in range(1, MAX_ROWS + 1):
-        o.append("template <>")
-        o.append("__device__ __forceinline__ void bsr_input_c<%d>(uint32_t (&acc)[%d][8], const uint32_t (&q)[30]," % (rt, rt))
-        o.append("                                               const uint64_t (&addr)[%d]) {" % rt)
-        o.append("    uint32_t keep;  // M0, saved and restored around the index-mode calls")
-        o.append("    asm volatile(")
-        o.append("        \"s_mov_b32 %%%d, m0\\n\\t\"" % (8 * rt))
-        nout = 8 * rt
-        for rr in range(rt):
-            if rr == 0:
-                o.append("        \"s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\\n\\t\"")
-            else:
-                o.append("        \"s_set_gpr_idx_idx %d\\n\\t\"" % (8 * rr))
-            o.append("        \"s_swappc_b64 s[30:31], %%%d\\n\\t\"" % (nout + 1 + 30 + rr))
-        o.append("        \"s_set_gpr_idx_off\\n\\t\"")
-        o.append("        \"s_mov_b32 m0, %%%d\\n\\t\"" % nout)
-        o.append("        \"s_nop 0\"")
-        outs = ['"+{v%d}"(acc[%d][%d])' % (ACC + 8 * rr + b, rr, b) for rr in range(rt) for b in range(8)]
-        outs.append('"=&s"(keep)')
-        ins = ['"{v%d}"(q[%d])' % (PL + d, d) for d in range(30)] + ['"s"(addr[%d])' % rr for rr in range(rt)]
-        o.append("        : " + ", ".join(outs))
-        o.append("        : " + ", ".join(ins))
-        o.append("        : \"s30\", \"s31\", \"scc\");")
-        o.append("}")
+    o.append("// instructions (index, call, return).  bsr_input_first<RT>: the wave's first")
+    o.append("// input, whose addresses are the set twins' (kBsrSetBase + 72 c).")
+    for name, cmb, first in (("bsr_input", False, False), ("bsr_input_first", False, True),
+                             ("bsr_input_c", True, False), ("bsr_input_c_first", True, True)):
+        if name == "bsr_input_c":
+            o.append("")
+            o.append("// bsr_input_c<RT>(acc, q, addr): the same with the input's 30 combinations (planes")
+            o.append("// and the 22 multi-plane XORs, in register order v%d..v%d) as inputs: built once per" % (PL, CB + 21))
+            o.append("// workgroup and read from LDS by every wave (matapply_bsr's combination-sharing")
+            o.append("// form), or built by the caller.")
+        src = "const uint32_t (&q)[30]" if cmb else "const uint32_t (&p)[8]"
+        o.append("template <int RT>")
+        o.append("__device__ __forceinline__ void %s(uint32_t (&acc)[RT][8], %s, const uint64_t (&addr)[RT]);"
+                 % (name, src))
+        for rt in range(1, MAX_ROWS + 1):
+            o.append("template <>")
+            o.append("__device__ __forceinline__ void %s<%d>(uint32_t (&acc)[%d][8], %s, const uint64_t (&addr)[%d]) {"
+                     % (name, rt, rt, src, rt))
+            statement(o, rt, cmb, first, form)
+            o.append("}")
     return "\n".join(o) + "\n"
 
 
 def main():
-    text = render()
+    form = sys.argv[sys.argv.index("--form") + 1] if "--form" in sys.argv else "vop2"
+    out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else OUT
+    text = render(form)
     if "--check" in sys.argv:
-        cur = open(OUT).read() if os.path.exists(OUT) else ""
+        cur = open(out).read() if os.path.exists(out) else ""
         sys.exit(0 if cur == text else 1)
-    with open(OUT, "w") as f:
+    with open(out, "w") as f:
         f.write(text)
 
 

@@ -15,6 +15,13 @@ against.
 
 With a --pmc counter_collection.csv (one row per dispatch and counter) it
 reports per-leg mean counter values instead of durations.
+
+Dispatches the library makes on its own, outside any launch bench.py records
+(INTERNAL: bsr_table_probe, the once-per-device read of the routine table's
+address before the first matapply_bsr launch), are skipped; any other name
+that differs from the recorded kernel is a pairing error: the script exits 1
+(round 5 paired every cfg3/cfg4 launch after the probe with its
+predecessor's leg).
 """
 import csv
 import json
@@ -39,6 +46,10 @@ def same(traced, recorded):
     nums = [a for a in ta if a.lstrip("-").isdigit()]
     rnums = [a for a in ra if a.lstrip("-").isdigit()]
     return nums[:len(rnums)] == rnums
+
+
+# library-internal dispatches: no leg of bench.py's records
+INTERNAL = ("bsr_table_probe",)
 
 
 def dispatches(path):
@@ -68,15 +79,20 @@ def dispatches(path):
 def main():
     legs = json.load(open(sys.argv[1]))
     rows = dispatches(sys.argv[2])
-    out, i, mismatch = {}, 0, 0
+    out, i, mismatch, skipped, first_bad = {}, 0, 0, 0, None
     for leg, kern, cnt in legs["legs"]:
         vals = []
         for _ in range(cnt):
+            while i < len(rows) and short(rows[i][1])[0] in INTERNAL and short(kern)[0] not in INTERNAL:
+                skipped += 1
+                i += 1
             if i >= len(rows):
                 break
             _, n, v = rows[i]
             if not same(n, kern):
                 mismatch += 1
+                if first_bad is None:
+                    first_bad = {"dispatch": i, "traced": n, "recorded": kern, "leg": leg}
             vals.append(v)
             i += 1
         if not vals:
@@ -84,7 +100,8 @@ def main():
         key = "%s | %s" % (leg, kern)
         out.setdefault(key, []).extend(vals)
     res = {"workload": legs.get("workload"), "source": sys.argv[2].split("/")[-1], "dispatches": len(rows),
-           "paired": i, "name_mismatches": mismatch, "legs": {}}
+           "paired": i, "internal_skipped": skipped, "name_mismatches": mismatch, "first_mismatch": first_bad,
+           "legs": {}}
     for key, vals in out.items():
         e = {"launches": len(vals)}
         for c in sorted(vals[0]):
@@ -100,6 +117,8 @@ def main():
         with open(sys.argv[3], "w") as f:
             f.write(txt + "\n")
     print(txt)
+    if mismatch:
+        sys.exit("trace_legs: %d dispatches do not match their recorded kernel (first: %s)" % (mismatch, first_bad))
 
 
 if __name__ == "__main__":

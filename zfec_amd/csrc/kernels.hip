@@ -895,8 +895,54 @@ __device__ __forceinline__ void bswap_blocks(uint32_t& a, uint32_t& b, int s, ui
     b = t1;
 }
 
-// 8 dwords (32 bytes) <-> 8 bit-planes; the transpose is its own inverse
+// Two block swaps with the same shift at once: the shifts on 64-bit register
+// pairs (v_lshlrev_b64 / v_lshrrev_b64 move two dwords at the issue cost of one
+// 32-bit shift, profiles/r02_mb_valu.log); the bits crossing the dword boundary
+// land where the swap's mask discards them.  Inline asm, or the compiler splits
+// the right shift back into v_alignbit + v_lshrrev.  (a0, a1) and (b0, b1) are
+// adjacent registers in the first two stages of transpose8 (the 16-byte loads
+// and the accumulator rows are register quads), so forming the pairs costs no
+// moves.  Same form as bitslice.cpp's sw2.
+__device__ __forceinline__ uint64_t vshl64(uint64_t x, int s) {
+    uint64_t r;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(s), "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint64_t vshr64(uint64_t x, int s) {
+    uint64_t r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(s), "v"(x));
+    return r;
+}
+__device__ __forceinline__ void bswap_blocks2(uint32_t& a0, uint32_t& b0, uint32_t& a1, uint32_t& b1, int s,
+                                              uint32_t m) {
+    const uint64_t bl = vshl64((static_cast<uint64_t>(b1) << 32) | b0, s);
+    const uint64_t ar = vshr64((static_cast<uint64_t>(a1) << 32) | a0, s);
+    const uint32_t t0 = bsel(m, a0, static_cast<uint32_t>(bl)), t1 = bsel(m, static_cast<uint32_t>(ar), b0);
+    const uint32_t t2 = bsel(m, a1, static_cast<uint32_t>(bl >> 32)), t3 = bsel(m, static_cast<uint32_t>(ar >> 32), b1);
+    a0 = t0;
+    b0 = t1;
+    a1 = t2;
+    b1 = t3;
+}
+
+// 8 dwords (32 bytes) <-> 8 bit-planes; the transpose is its own inverse.
+// ZFEC_TR64 (default): the first two stages on 64-bit shift pairs, 40 VOP3
+// instructions instead of 48 (tools/ab_bsr.sh, profiles/r06_bsr_ab.json).
+#ifndef ZFEC_TR64
+#define ZFEC_TR64 1
+#endif
 __device__ __forceinline__ void transpose8(uint32_t (&v)[8]) {
+#if ZFEC_TR64
+    bswap_blocks2(v[0], v[4], v[1], v[5], 4, 0x0F0F0F0Fu);
+    bswap_blocks2(v[2], v[6], v[3], v[7], 4, 0x0F0F0F0Fu);
+    bswap_blocks2(v[0], v[2], v[1], v[3], 2, 0x33333333u);
+    bswap_blocks2(v[4], v[6], v[5], v[7], 2, 0x33333333u);
+    bswap_blocks(v[0], v[1], 1, 0x55555555u);
+    bswap_blocks(v[2], v[3], 1, 0x55555555u);
+    bswap_blocks(v[4], v[5], 1, 0x55555555u);
+    bswap_blocks(v[6], v[7], 1, 0x55555555u);
+    return;
+#endif
     bswap_blocks(v[0], v[4], 4, 0x0F0F0F0Fu);
     bswap_blocks(v[1], v[5], 4, 0x0F0F0F0Fu);
     bswap_blocks(v[2], v[6], 4, 0x0F0F0F0Fu);
@@ -1135,9 +1181,25 @@ __global__ __launch_bounds__(256) void matapply_bsg(const J job) {
 //       of 8 on cfg4's first-seen decodes (profiles/r04_bsr_ab.json).
 // Coefficients: absolute routine addresses (BsrJob / BsrTblJob below).
 // ---------------------------------------------------------------------------
+// ZFEC_GF_ROUTINES_INC: another generated form of the routines (the A/B,
+// tools/ab_bsr.sh: `tools/gen_gf_routines.py --form legacy --out ...`)
+#ifdef ZFEC_GF_ROUTINES_INC
+#include ZFEC_GF_ROUTINES_INC
+#else
 #include "gf_routines.inc"
+#endif
 
 constexpr uint32_t kBsrChunk = 2048;  // bytes of each block per unit
+template <bool B>
+struct BoolC {  // a compile-time flag passed to generic lambdas
+    static constexpr bool value = B;
+};
+// ZFEC_BSR_EARLY_ADDR (default): the LDS-phase form loads the next input's
+// routine addresses before the current input's calls, not after them
+// (matapply_bsr; tools/ab_bsr.sh, profiles/r06_bsr_ab.json).
+#ifndef ZFEC_BSR_EARLY_ADDR
+#define ZFEC_BSR_EARLY_ADDR 1
+#endif
 typedef __attribute__((address_space(1))) void GlobalVoid;
 typedef __attribute__((address_space(3))) void LdsVoid;
 // Inputs per phase of the combination-sharing form (7.5 KiB of combinations +
@@ -1281,46 +1343,116 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
         const uint64_t ob = stripe * job.out_sstride + off + lane * 16u;
         uint32_t acc[RT][8];  // no zeroing: the wave's first input calls "set" routines (kBsrSetBase)
-        // the calls of one phase's kn inputs (ph, ph + 1, ...), planes or
-        // combinations at LDS offset o (u32x4): in pairs with fixed address
-        // registers (A: even, B: odd): after input j's calls its set is
-        // reloaded (scalar loads, unconditional: clamped to the phase's last
-        // input) with input j + 2's addresses, which have all of input j + 1 to
-        // arrive (one wait drains LDS and scalar loads alike)
-        auto calls = [&](uint32_t ph, uint32_t kn, uint32_t o) {
+        // One input's calls: its planes (or, CMB, its 30 combinations) read from
+        // LDS at b, its routine addresses in `cur`; the wave's first input
+        // (global index 0) calls the set twins (bsr_input_first: every row
+        // written).  `wait` runs between the LDS reads and the calls.
+        constexpr int kVals = CMB ? 30 : 8;
+        auto load = [&](const u32x4* b, uint32_t (&q)[kVals]) {
+            if constexpr (CMB) {
+#pragma unroll
+                for (int g = 0; g < 7; ++g) {
+                    const u32x4 t = b[g * 64 + lane];
+                    q[4 * g] = t.x;
+                    q[4 * g + 1] = t.y;
+                    q[4 * g + 2] = t.z;
+                    q[4 * g + 3] = t.w;
+                }
+                const u32x2 t2 = reinterpret_cast<const u32x2*>(b + 448)[lane];
+                q[28] = t2.x;
+                q[29] = t2.y;
+            } else {
+                const u32x4 pa = b[lane], pb = b[64u + lane];
+                q[0] = pa.x, q[1] = pa.y, q[2] = pa.z, q[3] = pa.w;
+                q[4] = pb.x, q[5] = pb.y, q[6] = pb.z, q[7] = pb.w;
+            }
+        };
+        auto input = [&](auto first, const uint32_t (&q)[kVals], const uint64_t (&cur)[RT]) {
+            if constexpr (CMB) {
+                if constexpr (decltype(first)::value)
+                    bsr_input_c_first<RT>(acc, q, cur);
+                else
+                    bsr_input_c<RT>(acc, q, cur);
+            } else {
+                if constexpr (decltype(first)::value)
+                    bsr_input_first<RT>(acc, q, cur);
+                else
+                    bsr_input<RT>(acc, q, cur);
+            }
+        };
+        // calls(first, ph, kn, o): the calls of one phase's kn inputs (ph, ph +
+        // 1, ...), planes or combinations at LDS offset o (u32x4).  The first
+        // phase is its own instance (first = BoolC<true>): its input 0 runs the
+        // set twins, peeled at compile time -- a run-time choice between the two
+        // statements made the compiler copy and spill the pinned accumulators.
+#if ZFEC_BSR_EARLY_ADDR
+        // Routine addresses, two sets by the parity of the input's global
+        // index (phases hold an even number of inputs: bsr_db_phase,
+        // bsr_cmb_phase).  Input g + 1's set is loaded (scalar loads) right
+        // after input g's LDS data has been waited for and before g's calls,
+        // so it arrives during them: the wait for g + 1's LDS data, which
+        // drains scalar loads too (lgkmcnt), finds it landed.  Round 5 loaded
+        // input g + 2's set after g's calls, and that wait stalled on it.
+        uint64_t ad0[RT], ad1[RT];
+        bsr_addrs<RT>(ad0, ca, 0);
+        auto step = [&](auto first, uint32_t gi, const u32x4* b, const uint64_t (&cur)[RT], uint64_t (&nxt)[RT]) {
+            uint32_t q[kVals];
+            load(b, q);
+            // a use of every value read: the LDS wait goes here, before the scalar loads
+            if constexpr (CMB)
+                asm volatile("" ::"v"(q[3]), "v"(q[7]), "v"(q[11]), "v"(q[15]), "v"(q[19]), "v"(q[23]), "v"(q[27]),
+                             "v"(q[29]));
+            else
+                asm volatile("" ::"v"(q[3]), "v"(q[7]));
+            __builtin_amdgcn_sched_barrier(0);
+            bsr_addrs<RT>(nxt, ca, gi + 1 < k ? gi + 1 : k - 1);  // unconditional (clamped)
+            __builtin_amdgcn_sched_barrier(0);
+            input(first, q, cur);
+        };
+        auto calls = [&](auto first, uint32_t ph, uint32_t kn, uint32_t o) {
+            uint32_t j = 0;
+            if constexpr (decltype(first)::value) {  // ph == 0
+                step(BoolC<true>{}, 0, bsr_planes + o, ad0, ad1);
+                for (j = 1; j + 1 < kn; j += 2) {
+                    step(BoolC<false>{}, j, bsr_planes + o + j * kIn, ad1, ad0);
+                    step(BoolC<false>{}, j + 1, bsr_planes + o + (j + 1) * kIn, ad0, ad1);
+                }
+                if (j < kn) step(BoolC<false>{}, j, bsr_planes + o + j * kIn, ad1, ad0);  // k < the phase
+                return;
+            }
+            for (; j + 1 < kn; j += 2) {
+                step(first, ph + j, bsr_planes + o + j * kIn, ad0, ad1);
+                step(first, ph + j + 1, bsr_planes + o + (j + 1) * kIn, ad1, ad0);
+            }
+            if (j < kn) step(first, ph + j, bsr_planes + o + j * kIn, ad0, ad1);  // the last phase
+        };
+#else
+        // In pairs with fixed address registers (A: even, B: odd): after input
+        // j's calls its set is reloaded (scalar loads, unconditional: clamped to
+        // the phase's last input) with input j + 2's addresses (round 5's schedule)
+        auto calls = [&](auto first, uint32_t ph, uint32_t kn, uint32_t o) {
             uint64_t ada[RT], adb[RT];
             bsr_addrs<RT>(ada, ca, ph);
             bsr_addrs<RT>(adb, ca, ph + (kn > 1 ? 1 : 0));
-            auto step = [&](uint32_t j, uint64_t (&ad)[RT]) {
-                const u32x4* b = bsr_planes + o + j * kIn;
-                if constexpr (CMB) {
-                    uint32_t q[30];
-#pragma unroll
-                    for (int g = 0; g < 7; ++g) {
-                        const u32x4 t = b[g * 64 + lane];
-                        q[4 * g] = t.x;
-                        q[4 * g + 1] = t.y;
-                        q[4 * g + 2] = t.z;
-                        q[4 * g + 3] = t.w;
-                    }
-                    const u32x2 t2 = reinterpret_cast<const u32x2*>(b + 448)[lane];
-                    q[28] = t2.x;
-                    q[29] = t2.y;
-                    bsr_input_c<RT>(acc, q, ad);
-                } else {
-                    const u32x4 pa = b[lane], pb = b[64u + lane];
-                    const uint32_t p[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-                    bsr_input<RT>(acc, p, ad);
-                }
+            auto step = [&](auto fst, uint32_t j, uint64_t (&ad)[RT]) {
+                uint32_t q[kVals];
+                load(bsr_planes + o + j * kIn, q);
+                input(fst, q, ad);
                 bsr_addrs<RT>(ad, ca, ph + (j + 2 < kn ? j + 2 : kn - 1));
             };
             uint32_t j = 0;
-            for (; j + 1 < kn; j += 2) {
-                step(j, ada);
-                step(j + 1, adb);
+            if constexpr (decltype(first)::value) {
+                step(BoolC<true>{}, 0, ada);
+                if (kn > 1) step(BoolC<false>{}, 1, adb);
+                j = 2;
             }
-            if (j < kn) step(j, ada);
+            for (; j + 1 < kn; j += 2) {
+                step(BoolC<false>{}, j, ada);
+                step(BoolC<false>{}, j + 1, adb);
+            }
+            if (j < kn) step(BoolC<false>{}, j, ada);
         };
+#endif
         if constexpr (!CMB) {
             // Planes: double-buffered phases of kq inputs.  A phase's inputs go
             // straight into LDS (LDS-DMA, global_load_lds: no registers in
@@ -1353,16 +1485,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             dma(0, kn, 0);
             xpose(kn, 0);
             __syncthreads();
-            for (uint32_t ph = 0; ph < k; ph += kq) {
+            auto phase = [&](auto first, uint32_t ph) {
                 const uint32_t nx = ph + kq, knx = nx < k ? (k - nx < kq ? k - nx : kq) : 0u;
                 const uint32_t ox = o ^ (kq * kIn);  // the other half
                 if (knx) dma(nx, knx, ox);
-                calls(ph, kn, o);
+                calls(first, ph, kn, o);
                 if (knx) xpose(knx, ox);
                 __syncthreads();  // phase ph's planes read, phase nx's written
                 kn = knx;
                 o = ox;
-            }
+            };
+            phase(BoolC<true>{}, 0);
+            for (uint32_t ph = kq; ph < k; ph += kq) phase(BoolC<false>{}, ph);
         } else {
             // Combinations: phases of kp = nw inputs, one per wave.  A phase's
             // inputs go into a raw staging area (LDS-DMA) while the waves walk
@@ -1398,17 +1532,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             dma(0, kn);
             build(kn);
             __syncthreads();
-            for (uint32_t ph = 0; ph < k; ph += kp) {
+            auto phase = [&](auto first, uint32_t ph) {
                 const uint32_t nx = ph + kp, knx = nx < k ? (k - nx < kp ? k - nx : kp) : 0u;
                 if (knx) dma(nx, knx);  // each wave's staging slot: read by its own build() before the barrier
-                calls(ph, kn, 0);
+                calls(first, ph, kn, 0);
                 __syncthreads();  // every wave has read the combinations before they are overwritten
                 if (knx) {
                     build(knx);
                     __syncthreads();
                 }
                 kn = knx;
-            }
+            };
+            phase(BoolC<true>{}, 0);
+            for (uint32_t ph = kp; ph < k; ph += kp) phase(BoolC<false>{}, ph);
         }
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
@@ -1453,10 +1589,13 @@ __device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uin
     // the loads and scalar loads are unconditional (past the last input they
     // re-read input n - 1, from L2): a conditional load would make the compiler
     // merge its registers with a copy that waits for every load in flight
-    auto step = [&](u32x4& x0, u32x4& x1, const uint8_t*& pn, uint64_t (&ad)[RT], uint32_t j) {
+    auto step = [&](auto first, u32x4& x0, u32x4& x1, const uint8_t*& pn, uint64_t (&ad)[RT], uint32_t j) {
         uint32_t p[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         transpose8(p);
-        bsr_input<RT>(acc, p, ad);
+        if constexpr (decltype(first)::value)  // the walk's first input: the set twins (fill_bsr_addrs)
+            bsr_input_first<RT>(acc, p, ad);
+        else
+            bsr_input<RT>(acc, p, ad);
         // input j + 2 into x0 / x1 / ad, which this input has consumed (after
         // the calls, so the compiler cannot keep the planes in them and copy)
         bsr_addrs<RT>(ad, ca, j + 2 < n ? j + 2 : n - 1);
@@ -1465,13 +1604,16 @@ __device__ __forceinline__ void bsr_walk(uint32_t (&acc)[RT][8], uint32_t n, uin
         pn = ptr(j + 4 < n ? j + 4 : n - 1);
     };
     // whole pairs, then an odd last input: with no conditional step inside the
-    // loop, input j's wait leaves input j + 1's loads in flight
-    uint32_t j = 0;
+    // loop, input j's wait leaves input j + 1's loads in flight.  Input 0 is
+    // peeled (the set twins, a statement of its own: a run-time choice between
+    // the two made the compiler copy the pinned accumulators).
+    step(BoolC<true>{}, a0, a1, pa, ada, 0);
+    uint32_t j = 1;
     for (; j + 1 < n; j += 2) {
-        step(a0, a1, pa, ada, j);
-        step(b0, b1, pb, adb, j + 1);
+        step(BoolC<false>{}, b0, b1, pb, adb, j);
+        step(BoolC<false>{}, a0, a1, pa, ada, j + 1);
     }
-    if (j < n) step(a0, a1, pa, ada, j);
+    if (j < n) step(BoolC<false>{}, b0, b1, pb, adb, j);
 }
 
 // One wave per (unit, row tile), no LDS: the wave loads and transposes every
@@ -2159,7 +2301,12 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 // with 2 or 4 the short phases cost more than the XORs saved (cfg4's first-seen
 // 20-row decode 0.439 -> 0.474 ms, 30/70 0.070 -> 0.074; profiles/r05_bsr_cmb_ab.json;
 // on DMA-staged phases 0.419 -> 0.428 and 0.065 -> 0.067, r05_lds_dma_ab.json).
-bool bsr_cmb(uint32_t nw) { return nw >= 8; }
+// ZFEC_BSR_CMB_MIN_NW: the least waves per workgroup that share combinations
+// (default 8; the A/B knob of tools/ab_build.sh)
+#ifndef ZFEC_BSR_CMB_MIN_NW
+#define ZFEC_BSR_CMB_MIN_NW 8
+#endif
+bool bsr_cmb(uint32_t nw) { return nw >= ZFEC_BSR_CMB_MIN_NW; }
 
 // LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations
 // and its raw staging, or two phases of planes (one when a single phase holds
@@ -2381,13 +2528,17 @@ bool bsr_tbl_ptrs(const ApplySpec& a, BsrTblJob& job) {
 // tiles of 9-10 when the launch has units for >= 16 waves per CU (cfg4's
 // 1024-stripe r = 20 decode: 0.469 ms, 3 tiles 0.475-0.48), else 4 tiles of 5
 // (one 64 MiB 20/40 stripe: 0.044 ms, 2 tiles 0.053, 3 tiles 0.048).
+// ZFEC_BSR_NW_WIDE: waves for r > 20 (default 4; the A/B knob of tools/ab_build.sh)
+#ifndef ZFEC_BSR_NW_WIDE
+#define ZFEC_BSR_NW_WIDE 4
+#endif
 void bsr_tiles(uint32_t r, uint64_t units, uint32_t* nw, uint32_t* rt) {
     if (r <= static_cast<uint32_t>(kBsrMaxRows))
         *nw = 1;
     else if (r <= 16 || (r <= 2u * kBsrMaxRows && units * 2 >= uint64_t(g_num_cu) * 16))
         *nw = 2;
     else
-        *nw = 4;
+        *nw = ZFEC_BSR_NW_WIDE;
     *rt = (r + *nw - 1) / *nw;
 }
 
