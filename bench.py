@@ -855,6 +855,11 @@ def run_batched_1mib(steps):
                     128-byte line partly written: HBM completes each such line
                     with a read-modify-write, 147 -> 161 us per launch,
                     profiles/r05_rowend_ab.json);
+      dense         a contiguous [256, 3, sz] tensor (blocks of exactly sz bytes
+                    back to back, no row slack: what Encoder.encode_batch gets
+                    from a caller who did not pad; easyfec's blocks,
+                    zfec/easyfec.py:28-39), outputs [256, 7, sz]: rows start
+                    and end mid-line;
       block-major   block j of every stripe back to back ([block][stripe][sz],
                     stripe stride = sz): fec_encode_batch runs it as ONE stripe
                     of 256 x sz bytes per block, 10 long streams.
@@ -873,12 +878,16 @@ def run_batched_1mib(steps):
                                           "workload's do (rows end on a whole 128-byte line inside their 256-byte "
                                           "padding); 'object-major, rows end mid-line': the same buffers without "
                                           "the flag (each output row's last line is written partially)")}
-    for layout in ("object-major", "object-major, rows end mid-line", "block-major"):
+    for layout in ("object-major", "object-major, rows end mid-line", "dense", "block-major"):
         flags = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if layout == "object-major" else 0)
         if layout.startswith("object-major"):
             fp = m * ld * ns
             shape_in, shape_out = (ns, k, ld), (ns, m - k, ld)
             sbs, sss, dbs, dss = ld, k * ld, ld, (m - k) * ld
+        elif layout == "dense":
+            fp = m * sz * ns
+            shape_in, shape_out = (ns, k, sz), (ns, m - k, sz)
+            sbs, sss, dbs, dss = sz, k * sz, sz, (m - k) * sz
         else:
             fp = m * sz * ns
             shape_in, shape_out = (k, ns * sz), (m - k, ns * sz)

@@ -43,7 +43,7 @@ def place(nums, k):
 # than 32 inputs in one kernel (94/100: benchmark-zfec/Main.hs:17); double-buffered LDS-DMA
 # phases of 4 with a short last one (14, 17, 30 inputs on 2 tiles, 23 on 3)
 JIT_SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (10, 58), (94, 100), (40, 48),
-              (14, 30), (17, 35), (23, 50), (30, 45)]
+              (14, 30), (17, 35), (23, 50), (30, 45), (30, 70)]
 
 
 @pytest.mark.parametrize("k,m", JIT_SHAPES)

@@ -38,10 +38,11 @@ def generated(tmp_path, monkeypatch, k, m, decode):
 
 
 # decodes from the last k blocks: r = 18 / 27 / 20 rows on 2 / 3 / 2 tiles, phases of 4 with a
-# short last one for k = 17 and 23
-@pytest.mark.parametrize("k,m", [(17, 35), (23, 50), (20, 60)])
-def test_dma_phase_structure(tmp_path, monkeypatch, k, m):
-    src = generated(tmp_path, monkeypatch, k, m, decode=True)
+# short last one for k = 17 and 23; 30/70's decode from its last 30 blocks: r = 30 on 3 tiles,
+# 8 phases (the last of 2)
+@pytest.mark.parametrize("k,m,decode", [(17, 35, True), (23, 50, True), (20, 60, True), (30, 70, True)])
+def test_dma_phase_structure(tmp_path, monkeypatch, k, m, decode):
+    src = generated(tmp_path, monkeypatch, k, m, decode=decode)
     size = int(re.search(r"__shared__ u32x4 sh\[(\d+)\]", src).group(1))
     assert size == 2 * 4 * 128, size  # two phases of 4 inputs, 128 u32x4 each
     # every DMA target and every plane access inside the declared LDS
@@ -62,10 +63,11 @@ def test_dma_phase_structure(tmp_path, monkeypatch, k, m):
         assert b.count("dma16(") >= 2 * (nphases - 1)
 
 
-def test_single_phase_kernel_keeps_register_loads(tmp_path, monkeypatch):
-    """K=20/M=60's r = 40 encode (4 tiles: all 20 inputs fit) loads through
-    registers in one phase; the DMA phases lost 2-8 % there
-    (profiles/r05_lds_dma_ab.json)."""
-    src = generated(tmp_path, monkeypatch, 20, 60, decode=False)
+@pytest.mark.parametrize("k,m", [(20, 60), (30, 70)])
+def test_single_phase_kernel_keeps_register_loads(tmp_path, monkeypatch, k, m):
+    """4-tile kernels (r = 40 encodes) load through registers in one phase of
+    all k inputs: DMA phases lost 2-8 % on K=20/M=60 (profiles/r05_lds_dma_ab.json)
+    and 2.3 % on 30/70 (profiles/r06_jit_dma_tiles_ab.json)."""
+    src = generated(tmp_path, monkeypatch, k, m, decode=False)
     assert "dma16(ka->" not in src and "dma_wait();" not in src
-    assert int(re.search(r"__shared__ u32x4 sh\[(\d+)\]", src).group(1)) == 20 * 128
+    assert int(re.search(r"__shared__ u32x4 sh\[(\d+)\]", src).group(1)) == k * 128

@@ -19,6 +19,12 @@ stripes / a column slice, or decode(encode(x)) == x):
   w94         94/100, one 64 MiB stripe, encode, JIT off (the ks form)
   cfg4_jit    cfg4_enc with the JIT as shipped after its compile (the
               compiled kernel: the reference point of cfg4_enc)
+  jit:K/M, bsr:K/M
+              K/M encode over 1024 x 1 MiB stripes, compiled (JIT) kernel /
+              JIT off
+  b1m_om / b1m_omp / b1m_dense / b1m_bm
+              the north-star batch, K=3/M=10 encode of 256 x 1 MiB stripes per
+              launch, in four layouts (batch_case)
 
     python tools/ab_bsr.py --variants r05,new --cases cfg4_enc,w128 --rounds 2 \\
         --out gpurun_out/ab.json
@@ -52,7 +58,15 @@ def worker(cases, launches):
         return ms, capi.last_kernel_name()
 
     for case in cases:
-        if case in ("cfg4_enc", "cfg4_dec", "cfg4_jit"):
+        if case.startswith("b1m_"):
+            res[case] = batch_case(case, launches, check)
+            continue
+        jit_case = case == "cfg4_jit" or case.startswith("jit:")
+        if case.startswith(("jit:", "bsr:")):  # K/M encode over 1024 x 1 MiB stripes
+            k, m = map(int, case[4:].split("/"))
+            ns = 1024
+            sz = -(-(1 << 20) // k)
+        elif case in ("cfg4_enc", "cfg4_dec", "cfg4_jit"):
             k, m, ns = 20, 60, 1024
             sz = -(-(1 << 20) // k)
         elif case == "w128":
@@ -66,7 +80,7 @@ def worker(cases, launches):
         r = m - k
         ld = (sz + 255) // 256 * 256
         code = capi.Code(k, m)
-        capi.jit_mode(capi.JIT_AUTO if case == "cfg4_jit" else capi.JIT_OFF)
+        capi.jit_mode(capi.JIT_AUTO if jit_case else capi.JIT_OFF)
         capi.generic_mode(2)
         nsets = max(2, -(-bench.COLD_SPAN // ((k + r) * ld * ns)))
         g = torch.Generator(device="cuda").manual_seed(k * 1000 + m)
@@ -121,6 +135,61 @@ def worker(cases, launches):
         del data, par
         torch.cuda.empty_cache()
     print("ABRESULT " + json.dumps(res), flush=True)
+
+
+def batch_case(case, launches, check):
+    """North-star batch (K=3/M=10 encode, 256 x 1 MiB stripes per launch) in one
+    layout: b1m_om object-major rows 256-byte aligned, no row-padding flag (rows
+    end mid-line); b1m_omp the same with FEC_FLAG_ROW_PADDING; b1m_dense a
+    contiguous [256, 3, sz] tensor (rows back to back, no slack: easyfec's
+    blocks, zfec/easyfec.py:28-39); b1m_bm block-major [3, 256 * sz]."""
+    import numpy as np
+    import torch
+
+    import bench
+    from oracle import oracle
+    from zfec_amd import capi
+
+    k, m, ns = 3, 10, 256
+    r = m - k
+    sz = -(-(1 << 20) // k)
+    ld = bench.row_stride(sz)
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream()
+    nums = list(range(k, m))
+    flags = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if case == "b1m_omp" else 0)
+    if case in ("b1m_om", "b1m_omp"):
+        shp_i, shp_o, sbs, sss, dbs, dss = (ns, k, ld), (ns, r, ld), ld, k * ld, ld, r * ld
+    elif case == "b1m_dense":
+        shp_i, shp_o, sbs, sss, dbs, dss = (ns, k, sz), (ns, r, sz), sz, k * sz, sz, r * sz
+    elif case == "b1m_bm":
+        shp_i, shp_o, sbs, sss, dbs, dss = (k, ns * sz), (r, ns * sz), ns * sz, sz, ns * sz, sz
+    else:
+        raise SystemExit("unknown case " + case)
+    fp = (shp_i[0] * shp_i[1] * shp_i[2]) + (shp_o[0] * shp_o[1] * shp_o[2]) if len(shp_i) == 3 else m * ns * sz
+    nsets = max(2, -(-bench.COLD_SPAN // fp))
+    src = [torch.randint(0, 256, shp_i, dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+    dst = [torch.empty(shp_o, dtype=torch.uint8, device="cuda") for _ in range(nsets)]
+
+    def enc_i(i):
+        def f(sh):
+            code.encode_batch(src[i].data_ptr(), sbs, sss, dst[i].data_ptr(), dbs, dss, nums, sz, ns, stream=sh,
+                              flags=flags)
+        return f
+
+    enc_i(0)(st.cuda_stream)
+    torch.cuda.synchronize()
+    if check:
+        flat_i, flat_o = src[0].reshape(-1), dst[0].reshape(-1)
+        for s_ in (0, 1, ns // 2, ns - 1):
+            blocks = np.stack([flat_i[s_ * sss + j * sbs:s_ * sss + j * sbs + sz].cpu().numpy() for j in range(k)])
+            got = np.stack([flat_o[s_ * dss + i * dbs:s_ * dss + i * dbs + sz].cpu().numpy() for i in range(r)])
+            assert np.array_equal(got, oracle.encode(k, m, blocks)), (case, s_)
+    cold, _ = bench.back_to_back([enc_i(i) for i in range(nsets)], launches, st, case)
+    kern = capi.last_kernel_name()
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"kernel": kern, "ms": round(cold, 4), "hbm_frac": round(ns * m * sz / (cold * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS, 4)}
 
 
 def main():

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Builds variant copies of libzfec_hip.so for kernel A/Bs, each in
-# abuild/<name>/ (git-ignored; travels to the GPU box with the tree).  Only
-# kernels.hip differs between variants; the other objects are the in-tree
-# build's (run `make` first).  A variant is
+# abuild/<name>/ (git-ignored; travels to the GPU box with the tree).
+# kernels.hip and bitslice.cpp (the JIT generator) are rebuilt per variant;
+# the other objects are the in-tree build's (run `make` first).  A variant is
 #
 #   name=FLAGS        kernels.hip of this tree with extra compiler flags, e.g.
 #                     "base=-DZFEC_TR64=0 -DZFEC_BSR_EARLY_ADDR=0 legacy"
@@ -20,7 +20,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS="--offload-arch=gfx950 -mcode-object-version=5 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function"
 SRC=$ROOT/zfec_amd/csrc
-OBJS="$SRC/fec_abi.o $SRC/gf256.o $SRC/bitslice.o $SRC/host_pool.o $SRC/config.o"
+OBJS="$SRC/fec_abi.o $SRC/gf256.o $SRC/host_pool.o $SRC/config.o"
 for o in $OBJS; do [ -f "$o" ] || { echo "ab_build: $o missing (run make)"; exit 1; }; done
 pids=()
 for spec in "$@"; do
@@ -52,9 +52,12 @@ for spec in "$@"; do
         fi
       done
       $HIPCC $FLAGS -I"$ROOT/include" "${extra[@]}" -c "$SRC/kernels.hip" -o "$out/kernels.o"
+      $HIPCC $FLAGS -I"$ROOT/include" "${extra[@]}" -c "$SRC/bitslice.cpp" -o "$out/bitslice.o"
     fi
-    $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$out/libzfec_hip.so" "$out/kernels.o" $OBJS -ldl -lpthread
-    rm -f "$out/kernels.o"
+    [ -f "$out/bitslice.o" ] || cp "$SRC/bitslice.o" "$out/bitslice.o"
+    $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$out/libzfec_hip.so" "$out/kernels.o" "$out/bitslice.o" $OBJS \
+      -ldl -lpthread
+    rm -f "$out/kernels.o" "$out/bitslice.o"
     echo "$spec" > "$out/SPEC"
     echo "built abuild/$name ($spec)"
   ) &

@@ -88,7 +88,7 @@ def masks(c):
     return out
 
 
-def routine(c, first=False, form="vop2"):
+def routine(c, first=False, form="vop2", slot=0):
     """Routine c adds c*x to the accumulator row (acc_b ^= L ^ H); with
     first=True it sets the row to c*x instead (acc_b = L ^ H), so a wave's
     first input needs no zeroed accumulators.  form "legacy": every plane a
@@ -98,12 +98,12 @@ def routine(c, first=False, form="vop2"):
     rest; the set twins run in DST-only index mode."""
     lines = []
     for b, (ml, mh) in enumerate(masks(c)):
-        acc = ACC + b
+        acc = ACC + 8 * slot + b  # slot: the row slot of the "slots" form (0 in the index-mode forms)
         if not ml and not mh and not first:
             continue
         sl = "v%d" % reg(0, ml) if ml else None
         sh = "v%d" % reg(1, mh) if mh else None
-        if form == "legacy":  # (trunc64: the vop2 instructions, cut below)
+        if form == "legacy":  # (trunc64, slots: the vop2 instructions; trunc64 cut below)
             lines.append("v_bitop3_b32 v%d, v%d, %s, %s bitop3:%s" % (acc, acc, sl or "0", sh or "0",
                                                                      "0x66" if first else "0x96"))
         elif first:
@@ -116,7 +116,8 @@ def routine(c, first=False, form="vop2"):
         else:
             lines.append("v_xor_b32 v%d, v%d, %s" % (acc, acc, sl or sh))
     if form == "trunc64":  # timing experiment only (wrong results): every routine cut to 64 bytes
-        # (form "inline": the statements run one fixed routine's body in place of each call)
+        # (form "inline": the statements run one fixed routine's body in place of each call;
+        # "noidx": the same without index mode, every row on row 0's registers)
         while routine_bytes(lines) + 4 > 64:
             lines.pop()
     lines.append("s_setpc_b64 s[30:31]")
@@ -135,9 +136,13 @@ def statement(o, rt, cmb, first, form):
     takes all 30 as inputs (bsr_input_c); first=True calls the set twins (the
     wave's first input), in DST-only index mode in the vop2 form."""
     mode = "gpr_idx(DST)" if first and form != "legacy" else "gpr_idx(SRC0,DST)"
+    slots = form == "slots"
     o.append("    uint32_t keep;  // M0, saved and restored around the index-mode calls")
     o.append("    asm volatile(")
-    o.append("        \"s_mov_b32 %%%d, m0\\n\\t\"" % (8 * rt))
+    if slots:  # no index mode: M0 untouched (keep stays an unused output)
+        o.append("        \"; %%%d\\n\\t\"" % (8 * rt))
+    else:
+        o.append("        \"s_mov_b32 %%%d, m0\\n\\t\"" % (8 * rt))
     if not cmb:
         for side in (0, 1):
             for m in MULTI:
@@ -146,20 +151,26 @@ def statement(o, rt, cmb, first, form):
     nout = 8 * rt
     nin = 8 if not cmb else 30
     for rr in range(rt):
-        if rr == 0:
+        if form in ("noidx", "slots"):  # (noidx: a timing experiment only, wrong results)
+            pass
+        elif rr == 0:
             o.append("        \"s_set_gpr_idx_on 0, %s\\n\\t\"" % mode)
         else:
             o.append("        \"s_set_gpr_idx_idx %d\\n\\t\"" % (8 * rr))
-        if form == "inline":  # timing experiment only (wrong results): a fixed routine's body, no call
+        if form in ("inline", "noidx"):  # timing experiment only (wrong results): a fixed routine's body, no call
             c = next(c for c in range(255, 0, -1) if all(ml and mh for ml, mh in masks(c)))
             for ln in routine(c, first=first, form="vop2")[:-1]:
                 o.append("        \"%s\\n\\t\"" % ln)
             o.append("        \"s_nop 0 ; %%%d\\n\\t\"" % (nout + 1 + nin + rr))
             continue
         o.append("        \"s_swappc_b64 s[30:31], %%%d\\n\\t\"" % (nout + 1 + nin + rr))
-    o.append("        \"s_set_gpr_idx_off\\n\\t\"")
-    o.append("        \"s_mov_b32 m0, %%%d\\n\\t\"" % nout)
-    o.append("        \"s_nop 0\"")
+    if form not in ("noidx", "slots"):
+        o.append("        \"s_set_gpr_idx_off\\n\\t\"")
+    if slots:
+        o.append("        \"\"")
+    else:
+        o.append("        \"s_mov_b32 m0, %%%d\\n\\t\"" % nout)
+        o.append("        \"s_nop 0\"")
     cons = "=" if first else "+"  # the set twins write every row they are called for
     outs = ['"%s{v%d}"(acc[%d][%d])' % (cons, ACC + 8 * rr + b, rr, b) for rr in range(rt) for b in range(8)]
     outs.append('"=&s"(keep)')
@@ -186,17 +197,22 @@ def render(form="vop2"):
     o.append("constexpr uint32_t kBsrStride = %d;   // bytes per routine" % stride)
     o.append("constexpr int kBsrMaxRows = %d;       // accumulator rows a wave can hold" % MAX_ROWS)
     o.append("constexpr uint32_t kBsrSetBase = %d;  // byte offset of the \"set\" routines (256 + c)" % (stride * 256))
+    nslot = MAX_ROWS if form == "slots" else 1
+    o.append("constexpr uint32_t kBsrSlotStride = %d;  // bytes per row slot's table (slots form; 0: index mode)"
+             % (stride * 512 if nslot > 1 else 0))
     # clang drops file-scope asm from device compilations: the table is the body
     # of a device function nothing calls (kept by `used`; its label is a symbol
     # of the code object the kernels' calls resolve against)
     o.append("extern \"C\" __device__ __attribute__((noinline, used)) void zfec_gf_routine_table() {")
-    o.append("asm volatile(\"s_branch zfec_gf_routines_end\\n\"")
+    # (a return, not a branch over the table: the slots form is past s_branch's +-128 KiB reach)
+    o.append("asm volatile(\"s_setpc_b64 s[30:31]\\n\"")
     o.append("    \".p2align 6\\n\"")
     o.append("    \"zfec_gf_routines:\\n\"")
-    for c in range(512):
-        o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * c))
-        o.append("    \"" + "\\n".join(routine(c % 256, first=c >= 256, form=form)) + "\\n\"")
-    o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * 512))
+    for rr in range(nslot):
+        for c in range(512):
+            o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * (512 * rr + c)))
+            o.append("    \"" + "\\n".join(routine(c % 256, first=c >= 256, form=form, slot=rr)) + "\\n\"")
+    o.append("    \".org zfec_gf_routines + %d\\n\"" % (stride * 512 * nslot))
     o.append("    \"zfec_gf_routines_end:\\n\");")
     o.append("}")
     o.append("")

@@ -22,7 +22,7 @@ def place(nums, k):
 
 # (k, m): tests/test_gpu_jit.py shapes, the auto-policy shape, bench cfg3 / cfg4, the wide-k shapes
 SHAPES = [(3, 10), (2, 40), (5, 9), (10, 16), (16, 32), (20, 60), (32, 40), (10, 58), (4, 12), (12, 21), (94, 100),
-          (40, 48), (255, 256), (14, 30), (17, 35), (23, 50), (30, 45)]
+          (40, 48), (255, 256), (14, 30), (17, 35), (23, 50), (30, 45), (30, 70)]
 
 
 def main():

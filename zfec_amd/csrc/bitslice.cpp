@@ -745,11 +745,19 @@ std::atomic<int> g_mode{-1};
 // keeps one register-loaded phase of all 20 inputs: phases of 8 lost 0.678-0.691
 // -> 0.665 of HBM, phases of 4 by DMA 0.600 -> 0.649 ms and one DMA phase
 // 0.600 -> 0.615 (profiles/r05_jit_phase_ab.json, r05_lds_dma_ab.json).
+// ZFEC_JIT_DMA_TILES_MAX (A/B knob, tools/ab_build.sh): the most row tiles a
+// kernel may have and still take DMA phases.  3: 4-tile kernels (e.g. 30/70's
+// r = 40 encode, 1024 x 1 MiB) keep one register-loaded phase of all k inputs,
+// 0.600-0.603 ms with DMA phases of 4 against 0.586-0.588
+// (profiles/r06_jit_dma_tiles_ab.json), as K=20/M=60's r = 40 encode does.
+#ifndef ZFEC_JIT_DMA_TILES_MAX
+#define ZFEC_JIT_DMA_TILES_MAX 3
+#endif
 BsOptions options_for(unsigned k, unsigned r) {
     BsOptions o;
     if (k > 32) o.share = false;
     const unsigned nt = bitslice_tiles(r, o);
-    o.phase = k * 2u * 12u > 160u * nt ? 4u : 0u;
+    o.phase = k * 2u * 12u > 160u * nt && nt <= ZFEC_JIT_DMA_TILES_MAX ? 4u : 0u;
     o.dma = o.phase && o.phase < k;
     return o;
 }

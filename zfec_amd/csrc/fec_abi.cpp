@@ -412,12 +412,12 @@ int classify(const gf* const* in, size_t nin, gf* const* out, size_t nout, Marsh
 // buffer's serial memcpy / DMA / kernel / DMA / memcpy (K=3/M=10 from bytes,
 // 1 MiB stripe: 137 vs 209 us per encode; 256 KiB stripe: 69 vs 77 us), but
 // not for many small blocks (K=20/M=60, 256 KiB stripe of 13 KB blocks: 260
-// vs 122 us; tools/host_lat_ab.py, profiles/r02_host_lat_ab.log).
+// vs 122 us; tools/archive/host_lat_ab.py, profiles/r02_host_lat_ab.log).
 constexpr size_t kStageMinBlock = size_t(64) << 10;
 // Up to Config::zc_limit bytes (1.5 MiB; calls of k <= 4, r <= 8 up to that
 // size stay on the bounce buffer, run_single) the kernel accesses the bounce
 // buffer in place.  Round 2 stopped at 256 KiB; an interleaved A/B of 100-150
-// KB K=3/M=10 stripes from bytes (tools/small_ab_inproc.py --set zc,
+// KB K=3/M=10 stripes from bytes (tools/archive/small_ab_inproc.py --set zc,
 // profiles/r03_zc_ab.log): encode 44.5-51.3 -> 25.1-33.0 us, decode
 // 17.0-38.3 -> 16.9-19.8 us against one H2D and one D2H copy.
 
@@ -778,7 +778,7 @@ int run_single(const uint8_t* coef, unsigned k, unsigned r, const gf* const* in,
     // and decode in 30-35 against 45-52; 512 KiB stripes (1.75 MB) encode
     // 78-97 against 84-86 us (box-dependent: staged from 1.5 MiB) and decode
     // (1.05 MB) 49-56 against 61 us; 1 MiB stripes 186 against 159 us
-    // (tools/small_ab_inproc.py --set stage, profiles/r03_stage_ab.log).
+    // (tools/archive/small_ab_inproc.py --set stage, profiles/r03_stage_ab.log).
     const bool zc_shape = k <= 4 && r <= 8;
     const size_t stage_from = zc_shape ? std::max(cfg.stage_min, cfg.zc_limit) : cfg.stage_min;
     if (sz * nhost > cfg.pack_limit || (sz * nhost > stage_from && sz >= kStageMinBlock))
@@ -1222,7 +1222,7 @@ void batch_geometry(unsigned k, unsigned r, size_t sbs, size_t sss, size_t dbs, 
     // strides leave room.  A row ending mid-line leaves a partly written line
     // that HBM completes with a read-modify-write: 10^6 K=3/M=10 stripes of
     // 1366-byte blocks in 1536-byte rows encode in 2.91 ms, of 1408-byte blocks
-    // in 2.55 ms (tools/grid_probe.py, profiles/r01_grid_probe_sz.log).
+    // in 2.55 ms (tools/archive/grid_probe.py, profiles/r01_grid_probe_sz.log).
     // `grant`: bytes past a row's start the flag lets us touch (per row).
     size_t grant = sz;
     if (flags & FEC_FLAG_ROW_PADDING) {

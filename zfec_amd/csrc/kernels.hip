@@ -220,6 +220,76 @@ struct UnitIter {
     }
 };
 
+// ZFEC_TAIL_ORDER (A/B knob, tools/ab_build.sh; 0 = UnitIter, the default):
+// where the register kernels' walk puts each stripe's last chunk (the one
+// that ends every row, mid-line when sz is not a multiple of 128): 1 = the
+// ns row-tail units first in the walk, then the rest in order; 2 = last.
+#ifndef ZFEC_TAIL_ORDER
+#define ZFEC_TAIL_ORDER 0
+#endif
+template <int ORDER>
+struct TailIter {
+    uint32_t s, c, g, step, ns, cpb, bq, br;  // cpb: body chunks per stripe (cps - 1)
+    template <class J>
+    __device__ TailIter(const J& job, uint32_t block) {
+        ns = job.nstripes;
+        cpb = job.cps - 1;
+        step = job.gs_s * job.cps + job.gs_c;
+        g = block * kBlock + threadIdx.x;
+        bq = cpb ? step / cpb : 0u;
+        br = cpb ? step - bq * cpb : 0u;
+        map();
+    }
+    __device__ void map() {
+        if (cpb == 0) {  // one chunk per stripe: no tail of its own
+            s = g;
+            c = 0;
+            return;
+        }
+        if constexpr (ORDER == 1) {
+            if (g < ns) {
+                s = g;
+                c = cpb;
+            } else {
+                const uint32_t h = g - ns;
+                s = h / cpb;
+                c = h - s * cpb;
+            }
+        } else {
+            const uint32_t body = ns * cpb;
+            if (g < body) {
+                s = g / cpb;
+                c = g - s * cpb;
+            } else {
+                s = g - body;
+                c = cpb;
+            }
+        }
+    }
+    template <class J>
+    __device__ __forceinline__ void next(const J&) {
+        const bool tail = cpb && c == cpb;
+        g += step;
+        if (cpb == 0 || tail || (ORDER == 2 && s + bq + 1 >= ns)) {  // regime change possible: recompute
+            map();
+            return;
+        }
+        c += br;
+        s += bq;
+        if (c >= cpb) {
+            c -= cpb;
+            ++s;
+        }
+        if constexpr (ORDER == 1)
+            if (s >= ns) s = 0xFFFFFFFFu;  // past the body: done
+    }
+};
+#if ZFEC_TAIL_ORDER
+using RegIter = TailIter<ZFEC_TAIL_ORDER>;
+#else
+using RegIter = UnitIter;
+#endif
+
 // Byte span of chunk c of a block of sz bytes.  Chunks are CH bytes; the last
 // one, when sz is not a multiple of CH, is shifted back to end at sz and so
 // overlaps its neighbour: both lanes compute and store identical bytes there,
@@ -348,14 +418,14 @@ __device__ __forceinline__ void reg_body(const RegJob<K, R>& job, uint32_t block
 
     const uint64_t sz = job.sz;
     const uint32_t nfull = static_cast<uint32_t>(sz / kChunk);
-    UnitIter u(job, block);
+    RegIter u(job, block);
     if constexpr (PF) {
         u32x4 x[K];
         Span sp = chunk_span<kChunk, true>(u.c, sz, nfull);
         uint64_t ob = u.s * job.out_sstride + sp.off;
         if (u.s < job.nstripes) reg_load<K, R>(job, x, u.s * job.in_sstride + sp.off, sp.full, sp.nb);
         while (u.s < job.nstripes) {
-            UnitIter v = u;
+            RegIter v = u;
             v.next(job);
             const Span spn = chunk_span<kChunk, true>(v.c, sz, nfull);
             u32x4 xn[K];
@@ -2194,12 +2264,7 @@ hipError_t ring_slot(TableRing** ring, unsigned* slot) {
     return hipSuccess;
 }
 
-// Whether `stream` is being captured into a HIP graph.  The table forms read a
-// device-side table the host fills (and reuses) at enqueue time: a captured
-// graph would replay its copy from a host slot rewritten since, and the bsr
-// address cache would hold a slot whose upload never ran (the copy is only
-// recorded).  Under capture those forms decline (hipErrorNotSupported) and a
-// kernel whose whole description travels in its arguments takes the launch.
+// matapply_bsg launch (the table form declines under graph capture: stream_capturing).
 hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsg_once, [] { fill_bsg<0>(); });
     const uint32_t k = a.k, r = a.r;
@@ -2340,40 +2405,66 @@ void fill_bsr() {
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
 }
 
-// The address of the routine table on each device, read once per device by
-// bsr_table_probe (the host writes every coefficient's routine address into the
-// launches' arguments).  A device whose probe fails gets no matapply_bsr
-// launches: launch_apply hands them to matapply_bsg.
+// The address of the routine table on each device, read by bsr_table_probe
+// (the host writes every coefficient's routine address into the launches'
+// arguments).  Only a successful probe is latched: a failed one (stream,
+// pinned buffer, launch or sync error) is reported on stderr under
+// ZFEC_HIP_JIT_VERBOSE and retried by a later launch, up to kBsrProbeTries per
+// device; until one succeeds the device gets no matapply_bsr launches
+// (launch_apply hands them to matapply_bsg).
 constexpr int kBsrMaxDevices = 64;
+constexpr int kBsrProbeTries = 3;
 struct BsrBase {
-    std::once_flag once;
-    std::atomic<bool> known{false};  // the probe has run (addr 0: it failed)
-    uint64_t addr = 0;
+    std::mutex mu;
+    std::atomic<uint64_t> addr{0};  // nonzero: the probe succeeded
+    int tries = 0;
 };
 BsrBase g_bsr_base[kBsrMaxDevices];
+
+hipError_t bsr_probe(uint64_t* addr) {
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    uint64_t* h = nullptr;
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(uint64_t), hipHostMallocDefault)) == hipSuccess) {
+        *h = 0;
+        hipLaunchKernelGGL(bsr_table_probe, dim3(1), dim3(64), 0, st, h);
+        if ((e = hipGetLastError()) == hipSuccess && (e = hipStreamSynchronize(st)) == hipSuccess)
+            *addr = *h;
+        (void)hipHostFree(h);
+    }
+    (void)hipStreamDestroy(st);
+    return e;
+}
 
 hipError_t bsr_routine_base(uint64_t* base, hipStream_t stream) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kBsrMaxDevices) return hipErrorNotSupported;
     BsrBase& b = g_bsr_base[dev];
-    // the probe synchronises a stream of its own: not while the launch stream is
-    // being captured into a graph (the launch declines; a later one probes)
-    if (!b.known.load(std::memory_order_acquire) && stream_capturing(stream)) return hipErrorNotSupported;
-    std::call_once(b.once, [&b] {
-        hipStream_t st = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return;
-        uint64_t* h = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void**>(&h), sizeof(uint64_t), hipHostMallocDefault) == hipSuccess) {
-            *h = 0;
-            hipLaunchKernelGGL(bsr_table_probe, dim3(1), dim3(64), 0, st, h);
-            if (hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess) b.addr = *h;
-            (void)hipHostFree(h);
+    uint64_t a = b.addr.load(std::memory_order_acquire);
+    if (!a) {
+        // the probe synchronises a stream of its own: not while the launch
+        // stream is being captured into a graph (the launch declines; a later one probes)
+        if (stream_capturing(stream)) return hipErrorNotSupported;
+        std::lock_guard<std::mutex> g(b.mu);
+        a = b.addr.load(std::memory_order_acquire);
+        if (!a && b.tries < kBsrProbeTries) {
+            ++b.tries;
+            uint64_t got = 0;
+            const hipError_t e = bsr_probe(&got);
+            if (e == hipSuccess && got) {
+                b.addr.store(got, std::memory_order_release);
+                a = got;
+            } else {
+                (void)hipGetLastError();
+                if (getenv("ZFEC_HIP_JIT_VERBOSE"))
+                    fprintf(stderr, "zfec_hip: routine-table probe on device %d failed (try %d of %d): %s\n", dev,
+                            b.tries, kBsrProbeTries, e == hipSuccess ? "address 0" : hipGetErrorString(e));
+            }
         }
-        (void)hipStreamDestroy(st);
-        b.known.store(true, std::memory_order_release);
-    });
-    if (!b.addr) return hipErrorNotSupported;
-    *base = b.addr;
+        if (!a) return hipErrorNotSupported;
+    }
+    *base = a;
     return hipSuccess;
 }
 
@@ -2399,9 +2490,9 @@ bool fill_bsr_addrs(uint64_t* dst, const ApplySpec& a, uint64_t base, uint32_t n
             uint64_t* d = dst + size_t(g * nw + w) * k * rt;
             for (uint32_t j = 0; j < k; ++j) {
                 const uint64_t tb = base + (first[j] ? kBsrSetBase : 0u);
-                for (uint32_t rr = 0; rr < rt; ++rr)
-                    d[size_t(j) * rt + rr] =
-                        tb + uint64_t(kBsrStride) * (rr < rows ? a.coef[size_t(r0 + rr) * a.coef_stride + j] : 0u);
+                for (uint32_t rr = 0; rr < rt; ++rr)  // (row slot rr's table in the slots form)
+                    d[size_t(j) * rt + rr] = tb + uint64_t(kBsrSlotStride) * rr +
+                                             uint64_t(kBsrStride) * (rr < rows ? a.coef[size_t(r0 + rr) * a.coef_stride + j] : 0u);
             }
         }
     }
@@ -2777,6 +2868,12 @@ void matapply_request_signal(uint32_t* flag_dev, uint32_t seq) {
 
 bool matapply_signal_used() { return t_signal_used; }
 
+// Whether `stream` is being captured into a HIP graph.  The table forms read a
+// device-side table the host fills (and reuses) at enqueue time: a captured
+// graph would replay its copy from a host slot rewritten since, and the bsr
+// address cache would hold a slot whose upload never ran (the copy is only
+// recorded).  Under capture those forms decline (hipErrorNotSupported) and a
+// kernel whose whole description travels in its arguments takes the launch.
 bool stream_capturing(hipStream_t stream) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
