@@ -184,20 +184,22 @@ def test_decode_rejects_what_reference_mishandles():
 
 def test_jit_prepare_compiles_without_gpu(tmp_path, monkeypatch):
     """fec_jit_prepare_encode / _decode generate and compile (hipRTC, gfx950)
-    the bit-sliced kernels a K=10/M=16 encode and a decode from blocks 6..15
-    would launch, and cache the code objects; no GPU involved."""
+    the bit-sliced kernels a K=11/M=17 encode and a decode from blocks 6..16
+    would launch, and cache the code objects; no GPU involved.  (A code no
+    other test compiles: the registry is per process, and fec_new's
+    prefetch loads the kernels of codes the in-tree cache holds.)"""
     monkeypatch.setenv("ZFEC_HIP_JIT_CACHE", str(tmp_path))
-    code = capi.Code(10, 16)
-    code.jit_prepare_encode(list(range(10, 16)))
-    code.jit_prepare_decode([10, 11, 12, 13, 14, 15, 6, 7, 8, 9])
-    files = sorted(tmp_path.glob("zfec_hip_bitslice_k10_r*.co"))
+    code = capi.Code(11, 17)
+    code.jit_prepare_encode(list(range(11, 17)))
+    code.jit_prepare_decode([11, 12, 13, 14, 15, 16, 6, 7, 8, 9, 10])
+    files = sorted(tmp_path.glob("zfec_hip_bitslice_k11_r*.co"))
     assert len(files) == 2, files
     for f in files:
         assert f.read_bytes()[:4] == b"\x7fELF"
-    code.jit_prepare_encode(list(range(10, 16)))  # in-memory hit: nothing new
+    code.jit_prepare_encode(list(range(11, 17)))  # in-memory hit: nothing new
     assert len(list(tmp_path.glob("*.co"))) == 2
     with pytest.raises(capi.FecError):
-        code.jit_prepare_decode([0, 0, 1, 2, 3, 4, 5, 6, 7, 8])  # duplicate: rejected before compiling
+        code.jit_prepare_decode([0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])  # duplicate: rejected before compiling
 
 
 @pytest.mark.skipif(zfec_amd.device_count() > 0, reason="only meaningful without a GPU")

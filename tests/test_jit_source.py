@@ -5,11 +5,14 @@ barriers, every LDS-DMA target and plane read stays inside the declared LDS,
 each wave waits for one DMA'd phase per phase of the matrix, and a kernel whose
 inputs all fit keeps its single register-loaded phase.  No GPU: the kernels are
 generated and compiled for gfx950 by hipRTC here."""
+import os
 import re
+import subprocess
+import sys
 
 import pytest
 
-from zfec_amd import capi
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def place(nums, k):
@@ -23,15 +26,20 @@ def place(nums, k):
 
 
 def generated(tmp_path, monkeypatch, k, m, decode):
-    monkeypatch.setenv("ZFEC_HIP_JIT_CACHE", str(tmp_path / "cache"))
+    """The generated source of the kernel of a K/M encode (all parity rows) or
+    decode (from the last k blocks), compiled in a fresh process: the JIT
+    registry is per process, and another test's code may already hold the
+    kernel in memory (fec_new prefetches the kernels the in-tree cache holds),
+    which would compile -- and dump -- nothing."""
     dump = tmp_path / "dump"
     dump.mkdir()
-    monkeypatch.setenv("ZFEC_HIP_JIT_DUMP", str(dump))
-    code = capi.Code(k, m)
-    if decode:
-        code.jit_prepare_decode(place(list(range(m - k, m)), k))
-    else:
-        code.jit_prepare_encode(list(range(k, m)))
+    env = dict(os.environ, ZFEC_HIP_JIT_CACHE=str(tmp_path / "cache"), ZFEC_HIP_JIT_DUMP=str(dump))
+    nums = place(list(range(m - k, m)), k) if decode else list(range(k, m))
+    prog = ("import sys; sys.path.insert(0, %r)\n"
+            "from zfec_amd import capi\n"
+            "c = capi.Code(%d, %d)\n"
+            "c.%s(%r)\n" % (ROOT, k, m, "jit_prepare_decode" if decode else "jit_prepare_encode", nums))
+    subprocess.run([sys.executable, "-c", prog], env=env, check=True, timeout=300)
     files = list(dump.glob("zfec_hip_bitslice_k%d_r*.hip" % k))
     assert len(files) == 1, files
     return files[0].read_text()

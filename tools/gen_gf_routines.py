@@ -155,9 +155,11 @@ def statement(o, rt, cmb, first, form):
             pass
         elif rr == 0:
             o.append("        \"s_set_gpr_idx_on 0, %s\\n\\t\"" % mode)
+        elif form == "inlinefix":  # timing experiment only: index mode on, never moved (every row on row 0)
+            pass
         else:
             o.append("        \"s_set_gpr_idx_idx %d\\n\\t\"" % (8 * rr))
-        if form in ("inline", "noidx"):  # timing experiment only (wrong results): a fixed routine's body, no call
+        if form in ("inline", "noidx", "inlinefix"):  # timing experiments (wrong results): a fixed body, no call
             c = next(c for c in range(255, 0, -1) if all(ml and mh for ml, mh in masks(c)))
             for ln in routine(c, first=first, form="vop2")[:-1]:
                 o.append("        \"%s\\n\\t\"" % ln)

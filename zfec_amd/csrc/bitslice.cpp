@@ -18,6 +18,7 @@
 // bytes and stored with streaming stores.
 #include "bitslice.hpp"
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -28,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <functional>
 #include <map>
 #include <memory>
@@ -783,35 +785,79 @@ std::string entry_key(const uint8_t* coef, unsigned k, unsigned r, const BsOptio
     return key;
 }
 
+std::string kernel_name(const std::string& key, unsigned k, unsigned r) {
+    char nm[80];
+    snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
+    return nm;
+}
+
+// A new registry entry (state 0, one pending) for `key`.  R.mu held.
+Entry* new_entry(const std::string& key, unsigned k, unsigned r, const BsOptions& opt) {
+    Registry& R = reg();
+    auto ne = std::make_unique<Entry>();
+    Entry* e = ne.get();
+    e->name = kernel_name(key, k, r);
+    const bool ks = bitslice_ksplit(k, r, opt);
+    e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
+    e->units_per_block = bitslice_split(r, opt) || ks ? 1 : 4;
+    R.entries.emplace(key, std::move(ne));
+    ++R.pending;
+    return e;
+}
+
+void spawn_worker(std::function<void()> f) {  // R.mu held
+    Registry& R = reg();
+    if (!R.atexit_set) {
+        std::atexit(join_workers);
+        R.atexit_set = true;
+    }
+    R.workers.emplace_back(std::move(f));
+}
+
 Entry* get_entry(const uint8_t* coef, unsigned k, unsigned r, bool sync, std::unique_lock<std::mutex>& lk) {
     Registry& R = reg();
     const BsOptions opt = options_for(k, r);
     const std::string key = entry_key(coef, k, r, opt);
     auto it = R.entries.find(key);
     if (it != R.entries.end()) return it->second.get();
-    auto ne = std::make_unique<Entry>();
-    Entry* e = ne.get();
-    char nm[80];
-    snprintf(nm, sizeof nm, "zfec_hip_bitslice_k%u_r%u_%016llx", k, r, static_cast<unsigned long long>(fnv1a(key)));
-    e->name = nm;
-    const bool ks = bitslice_ksplit(k, r, opt);
-    e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
-    e->units_per_block = bitslice_split(r, opt) || ks ? 1 : 4;
-    R.entries.emplace(key, std::move(ne));
-    ++R.pending;
+    Entry* e = new_entry(key, k, r, opt);
+    const char* nm = e->name.c_str();
     std::string src = bitslice_source(coef, k, r, opt, nm);
     if (sync) {
         lk.unlock();
         run_compile(e, std::move(src));
         lk.lock();
     } else {
-        if (!R.atexit_set) {
-            std::atexit(join_workers);
-            R.atexit_set = true;
-        }
-        R.workers.emplace_back(run_compile, e, std::move(src));
+        spawn_worker([e, s = std::move(src)]() mutable { run_compile(e, std::move(s)); });
     }
     return e;
+}
+
+// Names of the kernels whose code objects the disk cache holds (the part of a
+// file name before "-<source hash>.co"), read once per process and cache
+// directory: a code's construction (jit_prefetch) asks it, so it must cost a
+// lookup.
+bool on_disk(const std::string& name) {
+    static std::mutex mu;
+    static std::map<std::string, std::vector<std::string>> listed;
+    const std::string dir = cache_dir();
+    if (dir.empty()) return false;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = listed.find(dir);
+    if (it == listed.end()) {
+        std::vector<std::string> v;
+        if (DIR* d = opendir(dir.c_str())) {
+            while (dirent* de = readdir(d)) {
+                const std::string f = de->d_name;
+                const size_t dash = f.rfind('-');
+                if (dash != std::string::npos && f.size() > 3 && f.compare(f.size() - 3, 3, ".co") == 0)
+                    v.push_back(f.substr(0, dash));
+            }
+            closedir(d);
+        }
+        it = listed.emplace(dir, std::move(v)).first;
+    }
+    return std::find(it->second.begin(), it->second.end(), name) != it->second.end();
 }
 
 // The other kernels serve the rest: few coefficients (memory-bound), blocks
@@ -873,6 +919,22 @@ int jit_prepare(const uint8_t* coef, unsigned k, unsigned r) {
     Entry* e = get_entry(coef, k, r, true, lk);
     R.cv.wait(lk, [&] { return e->state != 0; });
     return e->state == 1 ? 0 : -1;
+}
+
+void jit_prefetch(const uint8_t* coef, unsigned k, unsigned r) {
+    if (jit_mode() != kJitAuto || k == 0 || r == 0 || k * r > kJitMaxCoef || k * r < 24 || (k <= 4 && r <= 8)) return;
+    const BsOptions opt = options_for(k, r);
+    std::string key = entry_key(coef, k, r, opt);
+    const std::string name = kernel_name(key, k, r);
+    if (!on_disk(name)) return;  // never compiled here: no compile
+    Registry& R = reg();
+    std::lock_guard<std::mutex> g(R.mu);
+    if (R.entries.count(key) || R.entries.size() >= kAutoMaxKernels) return;
+    Entry* e = new_entry(key, k, r, opt);
+    // the source (its hash names the cached file) is generated by the worker: ~10 ms at r = 40
+    spawn_worker([e, m = std::vector<uint8_t>(coef, coef + size_t(k) * r), k, r, opt]() {
+        run_compile(e, bitslice_source(m.data(), k, r, opt, e->name.c_str()));
+    });
 }
 
 int jit_wait() {

@@ -996,6 +996,10 @@ FEC_API void fec_init(void) {
     set_status(FEC_OK);
 }
 
+namespace {
+void prefetch_rows(const uint8_t* coef, unsigned k, unsigned r);  // below, with prepare_rows
+}
+
 FEC_API fec_t* fec_new(unsigned short k, unsigned short m) {
     if (!field_ready()) {  // zfec/fec.c:442-444
         set_status(FEC_EUNINIT, "fec_init() has not been called");
@@ -1019,6 +1023,10 @@ FEC_API fec_t* fec_new(unsigned short k, unsigned short m) {
     p->enc_matrix = enc;
     p->priv = nullptr;
     p->magic = magic_of(p);
+    // the full encode's compiled kernels, where an earlier process left them in
+    // the JIT disk cache: loaded in the background, so this code's first large
+    // encode can run them (bitslice.hpp jit_prefetch; no compile, no wait)
+    prefetch_rows(enc + size_t(k) * k, k, static_cast<unsigned>(m - k));
     set_status(FEC_OK);
     return p;
 }
@@ -1191,6 +1199,21 @@ int prepare_rows(const uint8_t* coef, unsigned k, unsigned r) {
             return set_status(FEC_EHIP, "JIT compile failed: %s", jit_last_error().c_str());
     }
     return set_status(FEC_OK);
+}
+}  // namespace
+
+namespace {
+// jit_prefetch for the row groups prepare_rows would compile.
+void prefetch_rows(const uint8_t* coef, unsigned k, unsigned r) {
+    if (r == 0) return;
+    const bool wide = k > static_cast<unsigned>(kMaxIn);
+    const unsigned rmax =
+        wide ? static_cast<unsigned>(kMaxOut) : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / k));
+    const unsigned ngroups = (r + rmax - 1) / rmax;
+    for (unsigned g = 0; g < ngroups; ++g) {
+        const unsigned i0 = g * r / ngroups, rg = (g + 1) * r / ngroups - i0;
+        if (k * rg <= kJitMaxCoef) jit_prefetch(coef + size_t(i0) * k, k, rg);
+    }
 }
 }  // namespace
 
