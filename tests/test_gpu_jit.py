@@ -129,10 +129,11 @@ def test_jit_all_primaries_flag(force_jit):
 def test_jit_auto_policy_background_compile():
     """Auto mode: the second large launch of a matrix queues its compile (both
     run the table kernel); after fec_jit_wait the specialised kernel runs;
-    same bytes."""
+    same bytes.  (13/22: a code whose kernel is not in the in-tree disk cache,
+    so fec_new prefetches nothing.)"""
     prev = capi.jit_mode(capi.JIT_AUTO)
     try:
-        k, m, sz = 12, 21, 4 << 20  # (k + r) * sz = 84 MiB per launch: above the auto threshold
+        k, m, sz = 13, 22, 4 << 20  # (k + r) * sz = 88 MiB per launch: above the auto threshold
         g = torch.Generator(device="cuda").manual_seed(12)
         data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda", generator=g)
         enc = zfec_amd.Encoder(k, m)
@@ -150,6 +151,27 @@ def test_jit_auto_policy_background_compile():
             assert bool(torch.equal(a, b))
         lo, hi = sz // 3, sz // 3 + 50000
         par = torch.stack(out2[k:])[:, lo:hi].cpu().numpy()
+        assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all()
+    finally:
+        capi.jit_mode(prev)
+
+
+def test_jit_prefetch_first_launch():
+    """Auto mode, a code whose compiled encode kernel an earlier process left
+    in the disk cache (tools/jit_warm.py compiled 12/21's into
+    zfec_amd/jit_cache/): fec_new loads it and its module in the background,
+    so the code's FIRST large encode runs it; bytes equal the oracle's."""
+    prev = capi.jit_mode(capi.JIT_AUTO)
+    try:
+        k, m, sz = 12, 21, 4 << 20
+        g = torch.Generator(device="cuda").manual_seed(1221)
+        data = torch.randint(0, 256, (k, sz), dtype=torch.uint8, device="cuda", generator=g)
+        enc = zfec_amd.Encoder(k, m)
+        capi.jit_wait()  # the prefetch (a file read and a module load: no compile)
+        out = enc.encode([data[i] for i in range(k)])
+        assert capi.last_kernel_name().startswith("zfec_hip_bitslice_k12_r9"), capi.last_kernel_name()
+        lo, hi = sz // 2, sz // 2 + 40000
+        par = torch.stack(out[k:])[:, lo:hi].cpu().numpy()
         assert (par == oracle.encode(k, m, data[:, lo:hi].cpu().numpy())).all()
     finally:
         capi.jit_mode(prev)

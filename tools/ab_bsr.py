@@ -17,6 +17,7 @@ stripes / a column slice, or decode(encode(x)) == x):
   w128        128/256, one 64 MiB stripe, encode of all 128 parity rows, JIT
               off (matapply_bsr<8,lds,tbl,cmb>)
   w94         94/100, one 64 MiB stripe, encode, JIT off (the ks form)
+  wide:K/M    K/M, one 64 MiB stripe, encode, JIT off
   cfg4_jit    cfg4_enc with the JIT as shipped after its compile (the
               compiled kernel: the reference point of cfg4_enc)
   jit:K/M, bsr:K/M
@@ -69,8 +70,9 @@ def worker(cases, launches):
         elif case in ("cfg4_enc", "cfg4_dec", "cfg4_jit"):
             k, m, ns = 20, 60, 1024
             sz = -(-(1 << 20) // k)
-        elif case == "w128":
-            k, m, ns = 128, 256, 1
+        elif case == "w128" or case.startswith("wide:"):  # one 64 MiB stripe, JIT off
+            k, m = (128, 256) if case == "w128" else map(int, case[5:].split("/"))
+            ns = 1
             sz = -(-(64 << 20) // k)
         elif case == "w94":
             k, m, ns = 94, 100, 1

@@ -687,6 +687,8 @@ struct Entry {
     unsigned units_per_block = 4;    // units a workgroup covers per loop trip
     std::vector<char> code;
     std::map<int, Loaded> dev;
+    int loading = -1;  // the device a prefetch worker is loading the module on
+    unsigned k = 0, r = 0;
 };
 
 struct Registry {
@@ -797,12 +799,57 @@ Entry* new_entry(const std::string& key, unsigned k, unsigned r, const BsOptions
     auto ne = std::make_unique<Entry>();
     Entry* e = ne.get();
     e->name = kernel_name(key, k, r);
+    e->k = k;
+    e->r = r;
     const bool ks = bitslice_ksplit(k, r, opt);
     e->threads = bitslice_split(r, opt) ? 64 * bitslice_tiles(r, opt) : 256;
     e->units_per_block = bitslice_split(r, opt) || ks ? 1 : 4;
     R.entries.emplace(key, std::move(ne));
     ++R.pending;
     return e;
+}
+
+// The module of a ready entry on device `dev` (the calling thread's current
+// device): hipModuleLoadData (~7 ms for K=20/M=60's r = 40 kernel,
+// tools/jit_load_probe.py), the function, its occupancy.
+hipError_t load_module(const Entry& e, int dev, Loaded& nl) {
+    hipError_t er = hipModuleLoadData(&nl.mod, e.code.data());
+    if (er == hipSuccess) er = hipModuleGetFunction(&nl.fn, nl.mod, e.name.c_str());
+    if (er != hipSuccess) {
+        (void)hipGetLastError();
+        return er;
+    }
+    int nb = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nl.fn, static_cast<int>(e.threads), 0) == hipSuccess &&
+        nb > 0)
+        nl.blocks_per_cu = nb;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+        nl.num_cu = ncu;
+    return hipSuccess;
+}
+
+// One launch of a freshly loaded kernel with no work (nstripes = 0: every
+// wave leaves its unit loop before touching memory) on a stream of its own:
+// the runtime copies a module's code to the device at its first launch (~5 ms
+// for K=20/M=60's r = 40 kernel, tools/jit_load_probe.py), which a prefetch
+// must not leave to the caller's first launch.
+bool warm_launch(const Entry& e, const Loaded& L) {
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    uint64_t args[5 + kMaxWideIn + kMaxOut] = {};  // sz, strides 0; nstripes 0, cps 1; null block pointers
+    const uint32_t a32[4] = {0u, 1u, 0u, 1u};
+    std::memcpy(&args[3], a32, sizeof a32);
+    size_t size = (5 + e.k + e.r) * sizeof(uint64_t);  // struct Args of the generated source
+    void* conf[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    hipError_t er = hipModuleLaunchKernel(L.fn, 1, 1, 1, e.threads, 1, 1, 0, st, nullptr, conf);
+    if (er == hipSuccess) er = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (er != hipSuccess) (void)hipGetLastError();
+    return er == hipSuccess;
 }
 
 void spawn_worker(std::function<void()> f) {  // R.mu held
@@ -927,13 +974,32 @@ void jit_prefetch(const uint8_t* coef, unsigned k, unsigned r) {
     std::string key = entry_key(coef, k, r, opt);
     const std::string name = kernel_name(key, k, r);
     if (!on_disk(name)) return;  // never compiled here: no compile
+    int dev = -1, ndev = 0;  // the caller's current device, whose module the worker loads
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
     Registry& R = reg();
     std::lock_guard<std::mutex> g(R.mu);
     if (R.entries.count(key) || R.entries.size() >= kAutoMaxKernels) return;
     Entry* e = new_entry(key, k, r, opt);
-    // the source (its hash names the cached file) is generated by the worker: ~10 ms at r = 40
-    spawn_worker([e, m = std::vector<uint8_t>(coef, coef + size_t(k) * r), k, r, opt]() {
+    // the source (its hash names the cached file) is generated by the worker:
+    // ~10 ms at r = 40; then the module is loaded on `dev` (~7 ms), so the
+    // first launch there finds the kernel ready
+    e->loading = dev;  // until the worker is done, launches on dev keep to the other kernels
+    ++R.pending;       // the module load: jit_wait waits for it too
+    spawn_worker([e, m = std::vector<uint8_t>(coef, coef + size_t(k) * r), k, r, opt, dev]() {
         run_compile(e, bitslice_source(m.data(), k, r, opt, e->name.c_str()));
+        Loaded nl;
+        const bool ok = dev >= 0 && e->state == 1 && hipSetDevice(dev) == hipSuccess &&
+                        load_module(*e, dev, nl) == hipSuccess && warm_launch(*e, nl);
+        Registry& R = reg();
+        std::lock_guard<std::mutex> g(R.mu);
+        if (ok && !e->dev.count(dev)) e->dev.emplace(dev, nl);
+        else if (ok) (void)hipModuleUnload(nl.mod);
+        e->loading = -1;  // (a failed load: the launch path loads and reports)
+        --R.pending;
+        R.cv.notify_all();
     });
 }
 
@@ -997,24 +1063,16 @@ hipError_t launch_matapply_jit(const ApplySpec& a, hipStream_t stream, const cha
         }
         if (e->state != 1) return hipErrorNotSupported;
         auto it = e->dev.find(dev);
+        if (it == e->dev.end() && e->loading == dev && mode != kJitForce)
+            return hipErrorNotReady;  // a prefetch is loading it: no 7 ms load in a launch
         if (it == e->dev.end()) {
             Loaded nl;
-            hipError_t er = hipModuleLoadData(&nl.mod, e->code.data());
-            if (er == hipSuccess) er = hipModuleGetFunction(&nl.fn, nl.mod, e->name.c_str());
+            const hipError_t er = load_module(*e, dev, nl);
             if (er != hipSuccess) {
-                (void)hipGetLastError();
                 e->state = 2;
                 R.last_error = std::string("loading ") + e->name + ": " + hipGetErrorString(er);
                 return hipErrorNotSupported;
             }
-            int nb = 0;
-            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nl.fn, static_cast<int>(e->threads), 0) ==
-                    hipSuccess &&
-                nb > 0)
-                nl.blocks_per_cu = nb;
-            int ncu = 0;
-            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
-                nl.num_cu = ncu;
             it = e->dev.emplace(dev, nl).first;
         }
         L = it->second;

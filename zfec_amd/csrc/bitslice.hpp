@@ -76,8 +76,9 @@ int jit_prepare(const uint8_t* coef, unsigned k, unsigned r);
 
 // Auto mode, a code's construction (fec_new): if the disk cache already holds
 // the compiled kernel of this r x k matrix (an earlier process compiled it),
-// load it in the background -- no compile, nothing waits -- so the matrix's
-// first large launch can run it instead of the run-time-data kernel.
+// load it in the background -- no compile, nothing waits -- together with its
+// module on the calling thread's current device, so the matrix's first large
+// launch can run it instead of the run-time-data kernel.
 void jit_prefetch(const uint8_t* coef, unsigned k, unsigned r);
 
 // Launch the specialised kernel for the matrix application `a`.

@@ -1205,7 +1205,7 @@ int prepare_rows(const uint8_t* coef, unsigned k, unsigned r) {
 namespace {
 // jit_prefetch for the row groups prepare_rows would compile.
 void prefetch_rows(const uint8_t* coef, unsigned k, unsigned r) {
-    if (r == 0) return;
+    if (r == 0 || jit_mode() != kJitAuto) return;
     const bool wide = k > static_cast<unsigned>(kMaxIn);
     const unsigned rmax =
         wide ? static_cast<unsigned>(kMaxOut) : std::max<unsigned>(1, std::min<unsigned>(kMaxOut, kMaxCoef / k));

@@ -1270,6 +1270,14 @@ struct BoolC {  // a compile-time flag passed to generic lambdas
 #ifndef ZFEC_BSR_EARLY_ADDR
 #define ZFEC_BSR_EARLY_ADDR 1
 #endif
+// ZFEC_BSR_CMB_DB (A/B knob, tools/ab_build.sh; off): the combination-sharing
+// form double-buffers its phases (one barrier per phase, half the waves build
+// the next phase during the current one's calls).  It lost: 128/256 0.109 ->
+// 0.112 ms, 160/256 0.112 -> 0.119, 64/112 0.051 -> 0.054
+// (profiles/r06_bsr_cmb_db_ab.json).
+#ifndef ZFEC_BSR_CMB_DB
+#define ZFEC_BSR_CMB_DB 0
+#endif
 typedef __attribute__((address_space(1))) void GlobalVoid;
 typedef __attribute__((address_space(3))) void LdsVoid;
 // Inputs per phase of the combination-sharing form (7.5 KiB of combinations +
@@ -1568,6 +1576,60 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             phase(BoolC<true>{}, 0);
             for (uint32_t ph = kq; ph < k; ph += kq) phase(BoolC<false>{}, ph);
         } else {
+#if ZFEC_BSR_CMB_DB
+            // Combinations, double-buffered: phases of kp = nw / 2 inputs, two
+            // phases' combinations resident.  The waves are two halves of kp
+            // (one wave of each per SIMD); wave i of half h owns input i of the
+            // phases of parity h.  In phase p, half (p + 1) & 1 builds phase p +
+            // 1 (its inputs arrived by LDS-DMA during phase p - 1: transpose, 30
+            // combinations, into the other buffer) and half p & 1 starts the
+            // LDS-DMA of phase p + 2 into the raw slots phase p has vacated;
+            // then every wave runs phase p's calls; one barrier ends the phase.
+            // (Single-buffered: phases of nw inputs, a barrier, every wave
+            // building one input, a second barrier: the build stalled the calls.)
+            const uint32_t kp = nw / 2, half = wave >= kp ? 1u : 0u, wi = wave - half * kp;
+            const uint32_t ocmb = 0, oraw = 2 * kp * kIn;  // [2][kp] combinations, then [2][kp] raw inputs
+            auto nin = [&](uint32_t ph) { return ph < k ? (k - ph < kp ? k - ph : kp) : 0u; };
+            auto dma = [&](uint32_t p) {  // my input of phase p into raw slot p & 1
+                if (wi < nin(p * kp)) {
+                    const uint8_t* ip = in_ptr(p * kp + wi) + ib;
+                    u32x4* b = bsr_planes + oraw + ((p & 1) * kp + wi) * 128u;
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip), (LdsVoid*)(b), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const GlobalVoid*)(ip + 1024), (LdsVoid*)(b + 64), 16, 0, 0);
+                }
+            };
+            auto build = [&](uint32_t p) {  // my input of phase p: raw slot -> combinations buffer p & 1
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as in the planes form)
+                if (wi < nin(p * kp)) {
+                    const u32x4* r = bsr_planes + oraw + ((p & 1) * kp + wi) * 128u;
+                    const u32x4 x0 = r[lane], x1 = r[64u + lane];
+                    uint32_t v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                    transpose8(v);
+                    uint32_t q30[30];
+                    bsr_combos(v, q30);
+                    u32x4* b = bsr_planes + ocmb + ((p & 1) * kp + wi) * kIn;
+#pragma unroll
+                    for (int g = 0; g < 7; ++g)
+                        b[g * 64 + lane] = u32x4{q30[4 * g], q30[4 * g + 1], q30[4 * g + 2], q30[4 * g + 3]};
+                    reinterpret_cast<u32x2*>(b + 448)[lane] = u32x2{q30[28], q30[29]};
+                }
+            };
+            const uint32_t np = (k + kp - 1) / kp;  // phases
+            dma(half);                              // phase 0 (half 0), phase 1 (half 1)
+            if (half == 0) build(0);
+            __syncthreads();
+            auto phase = [&](auto first, uint32_t p) {
+                if (half == ((p + 1) & 1)) {
+                    if (p + 1 < np) build(p + 1);
+                } else if (p + 2 < np) {
+                    dma(p + 2);
+                }
+                calls(first, p * kp, nin(p * kp), ocmb + (p & 1) * kp * kIn);
+                __syncthreads();  // phase p read, phase p + 1 written
+            };
+            phase(BoolC<true>{}, 0);
+            for (uint32_t p = 1; p < np; ++p) phase(BoolC<false>{}, p);
+#else
             // Combinations: phases of kp = nw inputs, one per wave.  A phase's
             // inputs go into a raw staging area (LDS-DMA) while the waves walk
             // the previous phase; after the barrier that ends it, each wave
@@ -1615,6 +1677,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             };
             phase(BoolC<true>{}, 0);
             for (uint32_t ph = kp; ph < k; ph += kp) phase(BoolC<false>{}, ph);
+        #endif
         }
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
@@ -2371,12 +2434,18 @@ hipError_t launch_bsg(const ApplySpec& a, hipStream_t stream) {
 #ifndef ZFEC_BSR_CMB_MIN_NW
 #define ZFEC_BSR_CMB_MIN_NW 8
 #endif
-bool bsr_cmb(uint32_t nw) { return nw >= ZFEC_BSR_CMB_MIN_NW; }
+// (the double-buffered form needs an even phase, nw / 2 >= 2: the kernel's
+// routine-address sets alternate by input parity across phases)
+bool bsr_cmb(uint32_t nw) { return nw >= ZFEC_BSR_CMB_MIN_NW && (!ZFEC_BSR_CMB_DB || nw >= 4); }
 
 // LDS of an nw-wave LDS-phase launch over k inputs: one phase of combinations
 // and its raw staging, or two phases of planes (one when a single phase holds
 // all k).
 size_t bsr_lds_bytes(uint32_t k, uint32_t nw, bool cmb) {
+#if ZFEC_BSR_CMB_DB
+    // two phases of nw / 2 inputs: combinations and raw staging each
+    if (cmb) return size_t(2) * (nw / 2) * (bsr_in_bytes<true>() + bsr_in_bytes<false>());
+#endif
     const uint32_t ph = cmb ? bsr_cmb_phase(nw) : bsr_db_phase(nw);
     if (cmb) return size_t(k < ph ? k : ph) * (bsr_in_bytes<true>() + bsr_in_bytes<false>());  // + raw staging
     return size_t(k <= ph ? k : 2 * ph) * bsr_in_bytes<false>();
