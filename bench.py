@@ -278,7 +278,7 @@ def place(nums, k):
     return [s if s is not None else next(sec) for s in slots]
 
 
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 
 
 def pmc_traffic(workload, leg="encode cold"):

@@ -16,9 +16,12 @@ against.
 With a --pmc counter_collection.csv (one row per dispatch and counter) it
 reports per-leg mean counter values instead of durations.
 
-Dispatches the library makes on its own, outside any launch bench.py records
-(INTERNAL: bsr_table_probe, the once-per-device read of the routine table's
-address before the first matapply_bsr launch), are skipped; any other name
+Dispatches the library makes on its own, outside any launch bench.py records,
+are skipped: bsr_table_probe (the once-per-device read of the routine table's
+address before the first matapply_bsr launch) and the no-work one-workgroup
+launch with which a JIT prefetch warms a compiled kernel (fec_new,
+bitslice.cpp warm_launch: a zfec_hip_bitslice dispatch whose grid is one
+workgroup; a real launch of those kernels is thousands).  Any other name
 that differs from the recorded kernel is a pairing error: the script exits 1
 (round 5 paired every cfg3/cfg4 launch after the probe with its
 predecessor's leg).
@@ -48,12 +51,21 @@ def same(traced, recorded):
     return nums[:len(rnums)] == rnums
 
 
-# library-internal dispatches: no leg of bench.py's records
-INTERNAL = ("bsr_table_probe",)
+def internal(r):
+    """A library-internal dispatch (see the module docstring)."""
+    n = r["Kernel_Name"]
+    if "bsr_table_probe" in n:
+        return True
+    if "zfec_hip_bitslice" in n:
+        grid = r.get("Grid_Size") or r.get("Grid_Size_X")
+        wg = r.get("Workgroup_Size") or r.get("Workgroup_Size_X")
+        return grid is not None and wg is not None and int(grid) == int(wg)
+    return False
 
 
 def dispatches(path):
-    """[(order key, kernel name, {duration_us | counter: value})] of the zfec dispatches."""
+    """[(order key, kernel name, {duration_us | counter: value})] of the zfec dispatches
+    (library-internal ones named "internal:<name>")."""
     with open(path) as f:
         rd = list(csv.DictReader(f))
     if rd and "Counter_Name" in rd[0]:
@@ -61,6 +73,8 @@ def dispatches(path):
         for r in rd:
             if "zfec_hip" not in r["Kernel_Name"]:
                 continue
+            if internal(r):
+                r = dict(r, Kernel_Name="internal:" + r["Kernel_Name"])
             d = by.setdefault(int(r["Dispatch_Id"]), (r["Kernel_Name"], {}))
             d[1][r["Counter_Name"]] = d[1].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         return [(key, n, v) for key, (n, v) in sorted(by.items())]
@@ -68,6 +82,8 @@ def dispatches(path):
     for r in rd:
         n = r["Kernel_Name"]
         if "zfec_hip" in n:
+            if internal(r):
+                n = "internal:" + n
             t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
             # enqueue order (launches on two streams may start out of it)
             key = int(r["Dispatch_Id"]) if r.get("Dispatch_Id") else t0
@@ -83,7 +99,7 @@ def main():
     for leg, kern, cnt in legs["legs"]:
         vals = []
         for _ in range(cnt):
-            while i < len(rows) and short(rows[i][1])[0] in INTERNAL and short(kern)[0] not in INTERNAL:
+            while i < len(rows) and rows[i][1].startswith("internal:"):
                 skipped += 1
                 i += 1
             if i >= len(rows):
