@@ -319,7 +319,8 @@ def device_tree_hash():
 
 def _bsr_traced_name(printed):
     """The library's matapply_bsr names -> the kernels' demangled names:
-    <RT> one-wave form, <RT,lds> LDS-phase form, <RT,lds,tbl> its table form
+    <RT> one-wave form, <RT,lds> LDS-phase form, <RT,lds,a32> its 32-bit
+    argument form, <RT,lds,tbl> its table form
     (",cmb": the combination-sharing variant of either),
     <RT,ks,tbl> the input-split form (kernels.hip fill_bsr*)."""
     if not printed.startswith("matapply_bsr<"):
@@ -329,6 +330,8 @@ def _bsr_traced_name(printed):
     form = ",".join(a[1:])
     return {"": "matapply_bsr_solo<%s>" % rt, "lds": "matapply_bsr<%s, false, false, BsrJob>" % rt,
             "lds,cmb": "matapply_bsr<%s, false, true, BsrJob>" % rt,
+            "lds,a32": "matapply_bsr<%s, false, false, BsrJob32>" % rt,
+            "lds,a32,cmb": "matapply_bsr<%s, false, true, BsrJob32>" % rt,
             "lds,tbl": "matapply_bsr<%s, true, false, BsrTblJob>" % rt,
             "lds,tbl,cmb": "matapply_bsr<%s, true, true, BsrTblJob>" % rt,
             "ks,tbl": "matapply_bsr_ks<%s>" % rt}.get(form)

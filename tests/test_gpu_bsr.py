@@ -450,10 +450,11 @@ def test_bsr_past_grid_cap(bsr_only, k, m, sz, ns):
 
 # Routine addresses travel in the kernel arguments up to 432 of them (kernels.hip
 # kBsrArgAddrs: waves x inputs x rows per wave), past that in the cached
-# device-side table: 27/43 (2 waves x 27 inputs x 8 rows = 432) and 28/44 (448)
-# sit on either side; 20/60 encodes 40 rows (4 x 20 x 10 = 800, the table form).
+# device-side table (written by bsr_table_write on a matrix's first launch):
+# 27/43 (2 waves x 27 inputs x 8 rows = 432) and 28/44 (448) sit on either side;
+# 20/60 encodes 40 rows (4 x 20 x 10 = 800), 30/70 1200.
 @pytest.mark.parametrize("k,m,want", [(27, 43, "matapply_bsr<8,lds>"), (28, 44, "matapply_bsr<8,lds,tbl>"),
-                                      (20, 60, "matapply_bsr<10,lds,tbl>")])
+                                      (20, 60, "matapply_bsr<10,lds,tbl>"), (30, 70, "matapply_bsr<10,lds,tbl>")])
 def test_bsr_argument_and_table_forms(bsr_only, k, m, want):
     rng = np.random.default_rng(k * 7 + m)
     for sz in (2048, 5000, 9000):

@@ -18,6 +18,8 @@ stripes / a column slice, or decode(encode(x)) == x):
               off (matapply_bsr<8,lds,tbl,cmb>)
   w94         94/100, one 64 MiB stripe, encode, JIT off (the ks form)
   wide:K/M    K/M, one 64 MiB stripe, encode, JIT off
+  cfg4_fl     cfg4_enc as first launches: 6 new row orders, one launch each
+              between events (bench.py's first_launch_encode leg)
   cfg4_jit    cfg4_enc with the JIT as shipped after its compile (the
               compiled kernel: the reference point of cfg4_enc)
   jit:K/M, bsr:K/M
@@ -59,6 +61,9 @@ def worker(cases, launches):
         return ms, capi.last_kernel_name()
 
     for case in cases:
+        if case == "cfg4_fl":
+            res[case] = first_launch_case(check)
+            continue
         if case.startswith("b1m_"):
             res[case] = batch_case(case, launches, check)
             continue
@@ -137,6 +142,51 @@ def worker(cases, launches):
         del data, par
         torch.cuda.empty_cache()
     print("ABRESULT " + json.dumps(res), flush=True)
+
+
+def first_launch_case(check):
+    """cfg4's shape, K=20/M=60 encodes of 1024 x 1 MiB stripes in 6 row orders
+    the process has not launched (rotations of the 40 parity numbers: each a new
+    matrix), JIT off, one launch per order between HIP events (as bench.py's
+    first_launch_encode leg): the kernel and the host work of a first launch."""
+    import numpy as np
+    import torch
+
+    import bench
+    from oracle import oracle
+    from zfec_amd import capi
+
+    k, m, ns = 20, 60, 1024
+    r = m - k
+    sz = -(-(1 << 20) // k)
+    ld = (sz + 255) // 256 * 256
+    capi.jit_mode(capi.JIT_OFF)
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream()
+    data = torch.randint(0, 256, (ns, k, ld), dtype=torch.uint8, device="cuda")
+    par = torch.empty((ns, r, ld), dtype=torch.uint8, device="cuda")
+    nums = list(range(k, m))
+    rows = []
+    for i in range(7):
+        order = nums[i:] + nums[:i]
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(st)
+        code.encode_batch(data.data_ptr(), ld, k * ld, par.data_ptr(), ld, r * ld, order, sz, ns,
+                          stream=st.cuda_stream, flags=capi.FEC_FLAG_ASYNC)
+        b.record(st)
+        torch.cuda.synchronize()
+        if i:
+            rows.append(a.elapsed_time(b))
+        if check and i == 6:
+            for s_ in (0, ns - 1):
+                want = oracle.encode(k, m, data[s_, :, :sz].cpu().numpy(), order)
+                assert np.array_equal(par[s_, :, :sz].cpu().numpy(), want), s_
+    ms = float(np.mean(rows))
+    del data, par
+    torch.cuda.empty_cache()
+    return {"kernel": capi.last_kernel_name(), "ms": round(ms, 4),
+            "hbm_frac": round((k + r) * sz * ns / (ms * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS, 4)}
 
 
 def batch_case(case, launches, check):

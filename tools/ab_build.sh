@@ -10,6 +10,7 @@
 #                     tools/gen_gf_routines.py --form legacy; `form=NAME` any
 #                     other form, e.g. form=trunc64, a timing-only experiment)
 #   name=git:REV      kernels.hip, kernels.hpp and gf_routines.inc of commit REV
+#   "name=git:REV FLAGS"  the same with compiler flags (a knob of that commit)
 #
 # The library loads its variant with ZFEC_HIP_LIB=abuild/<name>/libzfec_hip.so
 # (zfec_amd/capi.py); tools/ab_bsr.py runs the variants interleaved.
@@ -33,13 +34,15 @@ for spec in "$@"; do
     set -e
     if [[ $val == git:* ]]; then
       rev=${val#git:}
+      gflags=""
+      if [[ $rev == *" "* ]]; then gflags=${rev#* }; rev=${rev%% *}; fi
       mkdir -p "$out/src"
       for f in kernels.hip kernels.hpp gf_routines.inc; do
         git -C "$ROOT" show "$rev:zfec_amd/csrc/$f" > "$out/src/$f"
       done
       cp "$SRC"/*.hpp "$out/src/" 2>/dev/null || true
       git -C "$ROOT" show "$rev:zfec_amd/csrc/kernels.hpp" > "$out/src/kernels.hpp"
-      $HIPCC $FLAGS -I"$ROOT/include" -c "$out/src/kernels.hip" -o "$out/kernels.o"
+      $HIPCC $FLAGS -I"$ROOT/include" $gflags -c "$out/src/kernels.hip" -o "$out/kernels.o"
     else
       extra=()
       for w in $val; do

@@ -33,6 +33,21 @@ def main():
         for lay, x in d.get("batched_1MiB", {}).get("layouts", {}).items():
             rows += [("batched_1MiB %s cold" % lay, x["ms_per_launch"]),
                      ("batched_1MiB %s warm" % lay, x["ms_per_launch_warm"])]
+        # single launches between events (the first-seen / first-launch legs): the
+        # events also hold a launch's host-side gaps, so these are reported, not
+        # counted in the back-to-back legs' largest deviation
+        single = []
+        fs = d.get("first_seen_decode") or {}
+        fl = d.get("first_launch_encode") or {}
+        for tag, leg, src in (("first_seen", "first-seen decode", fs), ("jit", "first-seen jit decode", fs),
+                              ("first_launch", "first-launch encode", fl), ("jit", "first-launch jit encode", fl)):
+            if tag in src:
+                single.append((leg, src[tag]["ms_mean"]))
+        for name, ms in single:
+            t = trace(name)
+            if t:
+                print("%s %-34s event %9.2f us  trace %9.2f us  ratio %.3f (single launches)" % (w, name, ms * 1e3, t,
+                                                                                             ms * 1e3 / t))
         for name, ms in rows:
             t = trace(name)
             ratio = ms * 1e3 / t

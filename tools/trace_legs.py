@@ -41,8 +41,31 @@ def short(name):
     return base, [a.strip() for a in args.rstrip(">").split(",")]
 
 
+def bsr_traced(recorded):
+    """The library's printed matapply_bsr names -> (traced base name, template
+    arguments): <RT> the one-wave form (matapply_bsr_solo<RT>), <RT,lds> /
+    <RT,lds,cmb> / <RT,lds,tbl> / <RT,lds,tbl,cmb> matapply_bsr<RT, TBL, CMB, J>,
+    <RT,ks,tbl> matapply_bsr_ks<RT> (kernels.hip fill_bsr*; bench.py
+    _bsr_traced_name)."""
+    a = recorded[len("matapply_bsr<"):-1].split(",")
+    rt, form = a[0], ",".join(a[1:])
+    return {"": ("matapply_bsr_solo", [rt]), "lds": ("matapply_bsr", [rt, "false", "false", "BsrJob"]),
+            "lds,cmb": ("matapply_bsr", [rt, "false", "true", "BsrJob"]),
+            "lds,a32": ("matapply_bsr", [rt, "false", "false", "BsrJob32"]),
+            "lds,a32,cmb": ("matapply_bsr", [rt, "false", "true", "BsrJob32"]),
+            "lds,tbl": ("matapply_bsr", [rt, "true", "false", "BsrTblJob"]),
+            "lds,tbl,cmb": ("matapply_bsr", [rt, "true", "true", "BsrTblJob"]),
+            "ks,tbl": ("matapply_bsr_ks", [rt])}.get(form)
+
+
 def same(traced, recorded):
     tb, ta = short(traced)
+    if recorded.startswith("matapply_bsr<"):
+        m = bsr_traced(recorded)
+        if m is None or tb != m[0] or len(ta) < len(m[1]):
+            return False
+        # template arguments equal; a job type matches its unqualified name
+        return all(t == w or (w.startswith("Bsr") and t.split("::")[-1] == w) for t, w in zip(ta, m[1]))
     rb, ra = short(recorded)
     if tb != rb:
         return False

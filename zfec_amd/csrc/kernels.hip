@@ -55,6 +55,7 @@
 #include <mutex>
 #include <unordered_map>
 #include <vector>
+#include <type_traits>
 #include <utility>
 
 namespace zfec_hip {
@@ -1270,6 +1271,15 @@ struct BoolC {  // a compile-time flag passed to generic lambdas
 #ifndef ZFEC_BSR_EARLY_ADDR
 #define ZFEC_BSR_EARLY_ADDR 1
 #endif
+// ZFEC_BSR_TBL_WRITER (A/B knob, tools/ab_build.sh; 0): 1 writes a new
+// matrix's device-side address table with a kernel from the launch's
+// arguments instead of copying it from pinned host memory.  Even: K=20/M=60
+// first launches of new matrices 0.829-0.848 against 0.818-0.850 ms between
+// events (profiles/r06_bsr_tblwrite_ab.json); the host's enqueue, not the copy,
+// separates them from the compiled kernel's.
+#ifndef ZFEC_BSR_TBL_WRITER
+#define ZFEC_BSR_TBL_WRITER 0
+#endif
 // ZFEC_BSR_CMB_DB (A/B knob, tools/ab_build.sh; off): the combination-sharing
 // form double-buffers its phases (one barrier per phase, half the waves build
 // the next phase during the current one's calls).  It lost: 128/256 0.109 ->
@@ -1321,6 +1331,65 @@ struct alignas(16) BsrTblJob {
     const uint8_t* ptr[kBsrTblPtrs];  // k input block pointers, then r output block pointers
 };
 static_assert(sizeof(BsrTblJob) <= 4096, "kernel arguments are limited to 4 KiB");
+
+// 32-bit argument form (LDS-phase kernel, one row group): block pointers and
+// the routine addresses' low halves in the kernel arguments, the high half
+// (the same for the whole routine table) once.  It holds twice the addresses
+// of BsrJob -- K=20/M=60's 40-row encode needs 800 -- so a first launch of a
+// new matrix copies no table to the device: the table form's upload (a
+// hipMemcpyAsync the kernel waits for) cost a first launch ~65 us between its
+// events (profiles/r06_bench_vs_trace.txt).
+constexpr int kBsr32Ptrs = 72;  // k + r block pointers
+struct alignas(16) BsrJob32 {
+    uint64_t sz, in_sstride, out_sstride;
+    uint32_t nstripes, k, r, cps, gs_c, gs_s;
+    uint32_t ngroups;  // 1
+    uint32_t addr_hi;  // high 32 bits of every routine address
+    const uint8_t* ptr[kBsr32Ptrs];
+    uint32_t addr[(4096 - 56 - 8 * kBsr32Ptrs) / 4];  // [wave][input][RT] low halves (56: the header)
+};
+[[maybe_unused]] constexpr int kBsr32Addrs = (4096 - 56 - 8 * kBsr32Ptrs) / 4;
+static_assert(sizeof(BsrJob32) <= 4096, "kernel arguments are limited to 4 KiB");
+typedef const __attribute__((address_space(4))) uint32_t* CU32;
+
+// Where a wave's routine addresses come from: 64-bit values (kernel arguments
+// or the device-side table) or the 32-bit argument form's low halves.
+struct Addr64 {
+    CU64 p;
+    template <int RT>
+    __device__ __forceinline__ void load(uint64_t (&ad)[RT], uint32_t j) const {
+        const CU64 q = p + static_cast<uint64_t>(j) * RT;
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) ad[rr] = q[rr];
+    }
+};
+struct Addr32 {
+    CU32 p;
+    uint32_t hi;
+    template <int RT>
+    __device__ __forceinline__ void load(uint64_t (&ad)[RT], uint32_t j) const {
+        const CU32 q = p + static_cast<uint64_t>(j) * RT;
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) ad[rr] = (static_cast<uint64_t>(hi) << 32) | q[rr];
+    }
+};
+
+// Writes a device-side routine-address table from its 32-bit low halves in the
+// kernel arguments (one workgroup; the high half is one value for the whole
+// table): a launch's upload of a new matrix's table without a host-to-device
+// copy (bsr_addr_table).
+constexpr int kBsrWriteMax = (4096 - 16) / 4;  // addresses per writer launch
+struct alignas(16) BsrWriteJob {
+    uint64_t* dst;
+    uint32_t n, hi;
+    uint32_t lo[kBsrWriteMax];
+};
+static_assert(sizeof(BsrWriteJob) <= 4096, "kernel arguments are limited to 4 KiB");
+__global__ __launch_bounds__(256) void bsr_table_write(const BsrWriteJob job) {
+    const KPtr<BsrWriteJob> kj = kernarg_job<BsrWriteJob>();
+    for (uint32_t i = threadIdx.x; i < job.n; i += 256)
+        job.dst[i] = (static_cast<uint64_t>(job.hi) << 32) | kj->lo[i];
+}
 
 // Reads input j's RT routine addresses (scalar loads).
 // (The row offset is added to a 64-bit pointer, so the loads share one
@@ -1392,15 +1461,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
     const uint32_t ns = job.nstripes;
     uint32_t ng = 1;
     KPtr<J> kj = kernarg_job<J>();
+    constexpr bool A32 = std::is_same<J, BsrJob32>::value;  // 32-bit argument form
+    constexpr bool PTR = TBL || A32;                         // block pointers in ptr[]
     if constexpr (TBL) ng = job.ngroups;
     auto in_ptr = [&](uint32_t j) -> const uint8_t* {
-        if constexpr (TBL)
+        if constexpr (PTR)
             return kj->ptr[j];
         else
             return kj->in[j];
     };
     auto out_ptr = [&](uint32_t i) -> uint8_t* {
-        if constexpr (TBL)
+        if constexpr (PTR)
             return const_cast<uint8_t*>(kj->ptr[k + i]);
         else
             return kj->out[i];
@@ -1411,11 +1482,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         const uint32_t g = TBL && ng > 1 ? s / ns : 0u, stripe = s - g * ns;
         const uint32_t gr0 = g * r / ng, grn = (g + 1) * r / ng - gr0;
         const uint32_t r0 = gr0 + wave * grn / nw, rows = gr0 + (wave + 1) * grn / nw - r0;
-        CU64 ca;
-        if constexpr (TBL)
-            ca = (CU64)job.addr + (g * nw + wave) * k * RT;
-        else
-            ca = (CU64)kj->addr + wave * k * RT;
+        auto ca = [&] {
+            if constexpr (A32)
+                return Addr32{(CU32)kj->addr + wave * k * RT, job.addr_hi};
+            else if constexpr (TBL)
+                return Addr64{(CU64)job.addr + (g * nw + wave) * k * RT};
+            else
+                return Addr64{(CU64)kj->addr + wave * k * RT};
+        }();
         uint64_t off = static_cast<uint64_t>(c) * kBsrChunk;
         if (off > sz - kBsrChunk) off = sz - kBsrChunk;  // the last unit ends at sz (overlapping its neighbour)
         const uint64_t ib = stripe * job.in_sstride + off + lane * 16u;
@@ -1472,7 +1546,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         // drains scalar loads too (lgkmcnt), finds it landed.  Round 5 loaded
         // input g + 2's set after g's calls, and that wait stalled on it.
         uint64_t ad0[RT], ad1[RT];
-        bsr_addrs<RT>(ad0, ca, 0);
+        ca.template load<RT>(ad0, 0);
         auto step = [&](auto first, uint32_t gi, const u32x4* b, const uint64_t (&cur)[RT], uint64_t (&nxt)[RT]) {
             uint32_t q[kVals];
             load(b, q);
@@ -1483,7 +1557,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
             else
                 asm volatile("" ::"v"(q[3]), "v"(q[7]));
             __builtin_amdgcn_sched_barrier(0);
-            bsr_addrs<RT>(nxt, ca, gi + 1 < k ? gi + 1 : k - 1);  // unconditional (clamped)
+            ca.template load<RT>(nxt, gi + 1 < k ? gi + 1 : k - 1);  // unconditional (clamped)
             __builtin_amdgcn_sched_barrier(0);
             input(first, q, cur);
         };
@@ -1510,13 +1584,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void m
         // the phase's last input) with input j + 2's addresses (round 5's schedule)
         auto calls = [&](auto first, uint32_t ph, uint32_t kn, uint32_t o) {
             uint64_t ada[RT], adb[RT];
-            bsr_addrs<RT>(ada, ca, ph);
-            bsr_addrs<RT>(adb, ca, ph + (kn > 1 ? 1 : 0));
+            ca.template load<RT>(ada, ph);
+            ca.template load<RT>(adb, ph + (kn > 1 ? 1 : 0));
             auto step = [&](auto fst, uint32_t j, uint64_t (&ad)[RT]) {
                 uint32_t q[kVals];
                 load(bsr_planes + o + j * kIn, q);
                 input(fst, q, ad);
-                bsr_addrs<RT>(ad, ca, ph + (j + 2 < kn ? j + 2 : kn - 1));
+                ca.template load<RT>(ad, ph + (j + 2 < kn ? j + 2 : kn - 1));
             };
             uint32_t j = 0;
             if constexpr (decltype(first)::value) {
@@ -2456,9 +2530,13 @@ struct BsrVariant {
     const void* fn = nullptr;
     const void* fn_cmb = nullptr;  // combination-sharing form (bsr_cmb)
     const void* fn_solo = nullptr;
+    const void* fn_a32 = nullptr;  // 32-bit argument form (BsrJob32)
+    const void* fn_a32_cmb = nullptr;
     char name[24] = "";
     char name_cmb[28] = "";
     char name_solo[32] = "";
+    char name_a32[28] = "";
+    char name_a32_cmb[32] = "";
 };
 BsrVariant g_bsr_var[kBsrMaxRows + 1];
 std::once_flag g_bsr_once;
@@ -2471,6 +2549,12 @@ void fill_bsr() {
     snprintf(g_bsr_var[RT].name_cmb, sizeof g_bsr_var[RT].name_cmb, "matapply_bsr<%d,lds,cmb>", RT);
     g_bsr_var[RT].fn_solo = reinterpret_cast<const void*>(matapply_bsr_solo<RT>);
     snprintf(g_bsr_var[RT].name_solo, sizeof g_bsr_var[RT].name_solo, "matapply_bsr<%d>", RT);
+#if !ZFEC_BSR_NO_A32  // (instantiated only for the A/B)
+    g_bsr_var[RT].fn_a32 = reinterpret_cast<const void*>(matapply_bsr<RT, false, false, BsrJob32>);
+    g_bsr_var[RT].fn_a32_cmb = reinterpret_cast<const void*>(matapply_bsr<RT, false, true, BsrJob32>);
+#endif
+    snprintf(g_bsr_var[RT].name_a32, sizeof g_bsr_var[RT].name_a32, "matapply_bsr<%d,lds,a32>", RT);
+    snprintf(g_bsr_var[RT].name_a32_cmb, sizeof g_bsr_var[RT].name_a32_cmb, "matapply_bsr<%d,lds,a32,cmb>", RT);
     if constexpr (RT < kBsrMaxRows) fill_bsr<RT + 1>();
 }
 
@@ -2663,7 +2747,23 @@ hipError_t bsr_addr_table(const ApplySpec& a, hipStream_t stream, uint64_t base,
     uint64_t* h = reinterpret_cast<uint64_t*>(c.host + i * BsrTblCache::kSlotBytes);
     uint8_t* d = c.dev + i * BsrTblCache::kSlotBytes;
     if (!fill_bsr_addrs(h, a, base, ng, nw, rt, split)) return hipErrorInvalidValue;
-    if ((e = hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, stream)) != hipSuccess) return e;
+    const uint32_t hi = static_cast<uint32_t>(h[0] >> 32);
+    bool one_hi = ZFEC_BSR_TBL_WRITER && n <= size_t(4) * kBsrWriteMax;
+    for (size_t x = 0; one_hi && x < n; ++x) one_hi = static_cast<uint32_t>(h[x] >> 32) == hi;
+    if (one_hi) {
+        // up to 4 writer launches (~4 KB of arguments each) instead of the copy
+        for (size_t x0 = 0; x0 < n; x0 += kBsrWriteMax) {
+            BsrWriteJob w;
+            w.dst = reinterpret_cast<uint64_t*>(d) + x0;
+            w.n = static_cast<uint32_t>(n - x0 < size_t(kBsrWriteMax) ? n - x0 : kBsrWriteMax);
+            w.hi = hi;
+            for (uint32_t x = 0; x < w.n; ++x) w.lo[x] = static_cast<uint32_t>(h[x0 + x]);
+            if ((e = launch_job(reinterpret_cast<const void*>(bsr_table_write), 1, 256, 0, stream, w)) != hipSuccess)
+                return e;
+        }
+    } else if ((e = hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, stream)) != hipSuccess) {
+        return e;
+    }
     if ((e = bsr_table_done(BsrTblRef{&c, i, nullptr}, stream)) != hipSuccess) return e;  // the upload is a reader too
     std::memcpy(c.dims[i], dims, sizeof dims);
     c.coef[i] = m;
@@ -2867,6 +2967,47 @@ hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
     return launch_bsr_lds_tbl(a, stream, base, ng, nw, (rpg + nw - 1) / nw);
 }
 
+// ZFEC_BSR_NO_A32 (A/B knob, tools/ab_build.sh; 1 = off): 0 puts launches of
+// 433-866 addresses on the 32-bit argument form.  It lost: K=20/M=60's 40-row
+// encode 0.69 -> 0.74 ms back to back (each address needs its 64-bit SGPR pair
+// assembled: ~20 more scalar instructions per input and wave), and its first
+// launches of new matrices too (profiles/r06_bsr_a32_ab.json); the table form
+// stays, its upload written by a kernel (bsr_table_write).
+#ifndef ZFEC_BSR_NO_A32
+#define ZFEC_BSR_NO_A32 1
+#endif
+
+// The LDS-phase kernel in its 32-bit argument form (BsrJob32): one row group of
+// nw waves of rt rows.
+hipError_t launch_bsr_a32(const ApplySpec& a, hipStream_t stream, uint64_t base, uint32_t nw, uint32_t rt,
+                          uint64_t units, uint64_t cps) {
+    const uint32_t k = a.k, r = a.r;
+    BsrJob32 job;
+    job.sz = a.sz;
+    job.in_sstride = a.in_sstride;
+    job.out_sstride = a.out_sstride;
+    job.nstripes = static_cast<uint32_t>(a.nstripes);
+    job.k = k;
+    job.r = r;
+    job.ngroups = 1;
+    job.addr_hi = static_cast<uint32_t>(base >> 32);
+    for (uint32_t j = 0; j < k; ++j) job.ptr[j] = a.in[j];
+    for (uint32_t i = 0; i < r; ++i) job.ptr[k + i] = a.out[i];
+    thread_local std::vector<uint64_t> full;
+    full.resize(size_t(nw) * k * rt);
+    if (!fill_bsr_addrs(full.data(), a, base, 1, nw, rt, 1)) return hipErrorInvalidValue;
+    for (size_t i = 0; i < full.size(); ++i) job.addr[i] = static_cast<uint32_t>(full[i]);
+    const uint64_t cap = uint64_t(g_num_cu) * 1024;
+    const uint32_t grid = static_cast<uint32_t>(units < cap ? units : cap);
+    job.cps = static_cast<uint32_t>(cps);
+    job.gs_s = static_cast<uint32_t>(grid / cps);
+    job.gs_c = static_cast<uint32_t>(grid % cps);
+    const bool cmb = bsr_cmb(nw);
+    t_last_kernel = cmb ? g_bsr_var[rt].name_a32_cmb : g_bsr_var[rt].name_a32;
+    return launch_job(cmb ? g_bsr_var[rt].fn_a32_cmb : g_bsr_var[rt].fn_a32, grid, 64 * nw,
+                      bsr_lds_bytes(k, nw, cmb), stream, job);
+}
+
 hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     std::call_once(g_bsr_once, [] { fill_bsr<1>(); });
     uint64_t base = 0;
@@ -2877,9 +3018,21 @@ hipError_t launch_bsr(const ApplySpec& a, hipStream_t stream) {
     uint32_t nw, rt;
     bsr_tiles(r, units, &nw, &rt);
     if (units >= (1ull << 32) - (1ull << 24)) return hipErrorInvalidValue;
-    // more addresses than the arguments hold (e.g. K=20/M=60's 40-row encode):
-    // the same kernel reading them from a device-side table
-    if (size_t(nw) * k * rt > static_cast<size_t>(kBsrArgAddrs)) return launch_bsr_lds_tbl(a, stream, base, 1, nw, rt);
+    // more addresses than the arguments hold as 64-bit values (e.g. K=20/M=60's
+    // 40-row encode, 800): their low halves in the arguments (BsrJob32) when
+    // they fit and the routine table's high half is one value; else the same
+    // kernel reading them from a device-side table
+    if (size_t(nw) * k * rt > static_cast<size_t>(kBsrArgAddrs)) {
+        const uint64_t top = base + uint64_t(kBsrSlotStride ? kBsrSlotStride * kBsrMaxRows : kBsrSetBase * 2);
+#if !ZFEC_BSR_NO_A32
+        if (nw > 1 && size_t(nw) * k * rt <= static_cast<size_t>(kBsr32Addrs) && k + r <= uint32_t(kBsr32Ptrs) &&
+            (base >> 32) == (top >> 32))
+            return launch_bsr_a32(a, stream, base, nw, rt, units, cps);
+#else
+        (void)top;
+#endif
+        return launch_bsr_lds_tbl(a, stream, base, 1, nw, rt);
+    }
     BsrJob job;
     job.sz = a.sz;
     job.in_sstride = a.in_sstride;
