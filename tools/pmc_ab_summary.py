@@ -27,6 +27,8 @@ def main():
                     n = r["Kernel_Name"]
                     if "zfec" not in n or "probe" in n:
                         continue
+                    if "bitslice" in r["Kernel_Name"] and r.get("Grid_Size") == r.get("Workgroup_Size"):
+                        continue  # a JIT prefetch's no-work warm launch (bitslice.cpp warm_launch)
                     d = disp.setdefault((n, r["Dispatch_Id"]), {})
                     d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             for (n, _), cv in disp.items():

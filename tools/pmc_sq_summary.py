@@ -36,6 +36,8 @@ def summarize(tag, workloads):
                 for r in csv.DictReader(f):
                     if "zfec" not in r["Kernel_Name"]:
                         continue
+                    if "bitslice" in r["Kernel_Name"] and r.get("Grid_Size") == r.get("Workgroup_Size"):
+                        continue  # a JIT prefetch's no-work warm launch (bitslice.cpp warm_launch)
                     n = r["Kernel_Name"].replace("zfec_hip::(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0]
                     agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
             for n, v in agg.items():

@@ -29,8 +29,10 @@ def per_kernel(path, value="Counter_Value"):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 n = r["Kernel_Name"]
-                if "zfec" not in n and "matapply" not in n:
+                if "zfec" not in n and "matapply" not in n or "probe" in n:
                     continue
+                if "bitslice" in n and r.get("Grid_Size") == r.get("Workgroup_Size"):
+                    continue  # a JIT prefetch's no-work warm launch (bitslice.cpp warm_launch)
                 agg[(n, r.get("Dispatch_Id"))][r["Counter_Name"]].append(float(r[value]))
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     for (n, _), cs in agg.items():
@@ -45,6 +47,8 @@ def trace_means(path):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 n = r["Kernel_Name"]
+                if "bitslice" in n and r.get("Grid_Size_X") == r.get("Workgroup_Size_X"):
+                    continue  # (the prefetch's warm launch)
                 if "zfec" in n or "matapply" in n:
                     d[n].append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9)
     return {n: (sum(v) / len(v), len(v)) for n, v in d.items()}

@@ -2764,7 +2764,9 @@ hipError_t bsr_addr_table(const ApplySpec& a, hipStream_t stream, uint64_t base,
     } else if ((e = hipMemcpyAsync(d, h, n * 8, hipMemcpyHostToDevice, stream)) != hipSuccess) {
         return e;
     }
-    if ((e = bsr_table_done(BsrTblRef{&c, i, nullptr}, stream)) != hipSuccess) return e;  // the upload is a reader too
+    // (no event for the upload itself: the launch that follows on this stream records
+    // the slot's event whether or not it is accepted, bsr_table_done, and that event
+    // completes after the upload -- one hipEventRecord less in a first launch)
     std::memcpy(c.dims[i], dims, sizeof dims);
     c.coef[i] = m;
     *ref = BsrTblRef{&c, i, reinterpret_cast<const uint64_t*>(d)};
@@ -2886,9 +2888,11 @@ hipError_t launch_bsr_wide(const ApplySpec& a, hipStream_t stream) {
     job.gs_s = static_cast<uint32_t>(grid / cps);
     job.gs_c = static_cast<uint32_t>(grid % cps);
     job.addr = t.dev;
-    if ((e = launch_job(g_bsr_ks[rt].fn, grid, 64 * nw, 0, stream, job)) != hipSuccess) return e;
+    e = launch_job(g_bsr_ks[rt].fn, grid, 64 * nw, 0, stream, job);
+    const hipError_t te = bsr_table_done(t, stream);  // also when the launch failed: the upload is a reader
+    if (e != hipSuccess) return e;
     t_last_kernel = g_bsr_ks[rt].name;
-    return bsr_table_done(t, stream);
+    return te;
 }
 
 // Table form of the LDS-phase kernel: k > 32 with more than one row tile, or
@@ -2949,11 +2953,11 @@ hipError_t launch_bsr_lds_tbl(const ApplySpec& a, hipStream_t stream, uint64_t b
     job.gs_c = static_cast<uint32_t>(grid % cps);
     job.addr = t.dev;
     const bool cmb = bsr_cmb(nw);
-    if ((e = launch_job(cmb ? g_bsr_tbl[rt].fn_cmb : g_bsr_tbl[rt].fn, grid, 64 * nw, bsr_lds_bytes(k, nw, cmb), stream,
-                        job)) != hipSuccess)
-        return e;
+    e = launch_job(cmb ? g_bsr_tbl[rt].fn_cmb : g_bsr_tbl[rt].fn, grid, 64 * nw, bsr_lds_bytes(k, nw, cmb), stream, job);
+    const hipError_t te = bsr_table_done(t, stream);  // also when the launch failed: the upload is a reader
+    if (e != hipSuccess) return e;
     t_last_kernel = cmb ? g_bsr_tbl[rt].name_cmb : g_bsr_tbl[rt].name;
-    return bsr_table_done(t, stream);
+    return te;
 }
 
 hipError_t launch_bsr_tbl(const ApplySpec& a, hipStream_t stream) {
