@@ -9,6 +9,7 @@
 set -e
 TAG=$1
 shift
+ROUND=${ROUND:-r06}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
@@ -25,12 +26,26 @@ for what in "$@"; do
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     stats)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d $OUT/stats -o st -- python3 $ROOT/bench.py --no-cpu > $OUT/stats_bench.json 2> $OUT/stats_bench.err) ;;
+        -d $OUT/stats -o st -- python3 $ROOT/bench.py --no-cpu > $OUT/stats_bench.json 2> $OUT/stats_bench.err)
+      # keep the --stats summary, drop the per-dispatch trace (gpurun copies back <= 64 MiB)
+      find $OUT/stats -name "*kernel_trace.csv" -delete ;;
     profile)
-      tools/profile_r02.sh $TAG/prof ;;
+      tools/profile_r02.sh $TAG/prof
+      # summarised here (the raw traces and counter dumps exceed gpurun's 64 MiB copy-back)
+      python3 tools/legs_summary.py $TAG/prof $ROUND > $OUT/legs_summary.log 2>&1 || true
+      python3 tools/bench_vs_trace.py $TAG/prof $ROUND > $OUT/${ROUND}_bench_vs_trace.txt 2>&1 || true
+      mkdir -p $OUT/summary
+      cp profiles/${ROUND}_legs_*.json profiles/${ROUND}_cfg*_kernel_stats.csv $OUT/summary/ || true
+      rm -rf $OUT/prof ;;
     pmc)
       for W in cfg2 cfg4 first_seen; do tools/pmc_sq.sh $W $TAG/sq; done
-      tools/pmc_wide.sh $TAG/wide ;;
+      tools/pmc_wide.sh $TAG/wide
+      python3 tools/pmc_sq_summary.py $TAG/sq $ROUND cfg2 cfg4 first_seen > $OUT/pmc_sq_summary.log 2>&1 || true
+      python3 tools/pmc_wide_summary.py $TAG/wide $ROUND > $OUT/pmc_wide_summary.log 2>&1 || true
+      mkdir -p $OUT/summary
+      cp profiles/pmc_sq_summary.json profiles/${ROUND}_pmc_sq.json profiles/${ROUND}_wide_rooflines.json $OUT/summary/ || true
+      find $OUT/wide/kt -name "*kernel_stats.csv" -exec cp {} $OUT/summary/${ROUND}_wide_kernel_stats.csv \;
+      rm -rf $OUT/sq $OUT/wide ;;
   esac
   echo "gpu_round $what done"
 done
