@@ -39,10 +39,10 @@ def main():
         single = []
         fs = d.get("first_seen_decode") or {}
         fl = d.get("first_launch_encode") or {}
-        for tag, leg, src in (("first_seen", "first-seen decode", fs), ("jit", "first-seen jit decode", fs),
+        for key, leg, src in (("first_seen", "first-seen decode", fs), ("jit", "first-seen jit decode", fs),
                               ("first_launch", "first-launch encode", fl), ("jit", "first-launch jit encode", fl)):
-            if tag in src:
-                single.append((leg, src[tag]["ms_mean"]))
+            if key in src:
+                single.append((leg, src[key]["ms_mean"]))
         for name, ms in single:
             t = trace(name)
             if t:
