@@ -736,6 +736,67 @@ def test_batch_row_padding_flag(k, m, sz, ns, ld, used):
     assert rv[:, :, pad:].sum() == 0
 
 
+def test_north_star_batch_layouts():
+    """The four calls bench.py's batched_1MiB leg times (K=3/M=10, 256 stripes
+    of 1 MiB, sz = 349,526 per block): object-major rows at a 256-byte stride
+    with FEC_FLAG_ROW_PADDING and without it, a dense [256, 3, sz] array and
+    block-major rows.  Every layout gives the same parity bytes for every
+    stripe, sampled stripes equal the oracle's, and nothing is written past
+    what each call may write: the padding past the 128-byte line (flag) or
+    past sz (no flag), and guard bytes after the dense and block-major
+    arrays."""
+    k, m, ns = 3, 10, 256
+    r, sz = m - k, -(-(1 << 20) // k)
+    ld, pad, g = -(-sz // 256) * 256, -(-sz // 128) * 128, 4096
+    rng = np.random.default_rng(2026)
+    data = rng.integers(0, 256, size=(ns, k, sz), dtype=np.uint8)
+    dev = torch.from_numpy(data).cuda()
+    code = capi.Code(k, m)
+    st = torch.cuda.current_stream().cuda_stream
+    nums = list(range(k, m))
+    outs = {}
+    for layout in ("object-major", "object-major, rows end mid-line", "dense", "block-major"):
+        flags = capi.FEC_FLAG_ASYNC | (capi.FEC_FLAG_ROW_PADDING if layout == "object-major" else 0)
+        if layout.startswith("object-major"):
+            src = torch.full((ns, k, ld), 0xA5, dtype=torch.uint8, device="cuda")
+            src[:, :, :sz] = dev
+            dst = torch.zeros((ns, r, ld), dtype=torch.uint8, device="cuda")
+            sbs, sss, dbs, dss = ld, k * ld, ld, r * ld
+        elif layout == "dense":
+            src = dev.clone()
+            flat = torch.zeros(ns * r * sz + g, dtype=torch.uint8, device="cuda")
+            dst = flat[:ns * r * sz].view(ns, r, sz)
+            sbs, sss, dbs, dss = sz, k * sz, sz, r * sz
+        else:
+            src = dev.transpose(0, 1).contiguous().view(k, ns * sz)
+            flat = torch.zeros(r * ns * sz + g, dtype=torch.uint8, device="cuda")
+            dst = flat[:r * ns * sz].view(r, ns * sz)
+            sbs, sss, dbs, dss = ns * sz, sz, ns * sz, sz
+        code.encode_batch(src.data_ptr(), sbs, sss, dst.data_ptr(), dbs, dss, nums, sz, ns, stream=st, flags=flags)
+        torch.cuda.synchronize()
+        assert capi.last_kernel_name().startswith("matapply_reg<3,7>"), (layout, capi.last_kernel_name())
+        if layout == "object-major":
+            assert int(dst[:, :, pad:].count_nonzero()) == 0, "written past the padded line"
+            view = dst[:, :, :sz]
+        elif layout.startswith("object-major"):
+            assert int(dst[:, :, sz:].count_nonzero()) == 0, "written past sz without the flag"
+            view = dst[:, :, :sz]
+        elif layout == "dense":
+            assert int(flat[ns * r * sz:].count_nonzero()) == 0, "written past the dense array"
+            view = dst
+        else:
+            assert int(flat[r * ns * sz:].count_nonzero()) == 0, "written past the block-major rows"
+            view = dst.view(r, ns, sz).transpose(0, 1)
+        outs[layout] = view
+        del src
+    first = outs["object-major"]
+    for layout, v in outs.items():
+        assert torch.equal(v, first), layout
+    got = first.cpu().numpy()
+    for s in sorted({0, 1, 127, 128, 255} | {int(x) for x in rng.integers(0, ns, 3)}):
+        assert (got[s] == oracle.encode(k, m, data[s])).all(), s
+
+
 @pytest.mark.parametrize("k,m,nums", [(3, 10, [7, 1, 9]), (5, 9, [0, 1, 2, 3, 4]), (10, 16, list(range(6, 16)))])
 def test_decode_all_primaries_flag(k, m, nums):
     """FEC_FLAG_ALL_PRIMARIES: the k outputs are the primaries in order, present ones copied."""
