@@ -17,6 +17,7 @@ stripes / a column slice, or decode(encode(x)) == x):
   w128        128/256, one 64 MiB stripe, encode of all 128 parity rows, JIT
               off (matapply_bsr<8,lds,tbl,cmb>)
   w94         94/100, one 64 MiB stripe, encode, JIT off (the ks form)
+  s64         K=3/M=10, one 64 MiB stripe, encode (cfg2's matapply_reg<3,7>)
   wide:K/M    K/M, one 64 MiB stripe, encode, JIT off
   cfg4_fl     cfg4_enc as first launches: 6 new row orders, one launch each
               between events (bench.py's first_launch_encode leg)
@@ -81,6 +82,9 @@ def worker(cases, launches):
             sz = -(-(64 << 20) // k)
         elif case == "w94":
             k, m, ns = 94, 100, 1
+            sz = -(-(64 << 20) // k)
+        elif case == "s64":  # cfg2's stripe: K=3/M=10, one 64 MiB stripe (matapply_reg<3,7>)
+            k, m, ns = 3, 10, 1
             sz = -(-(64 << 20) // k)
         else:
             raise SystemExit("unknown case " + case)
