@@ -147,8 +147,9 @@ def parse():
     p.add_argument("--streams", type=int, default=None, choices=[1, 2],
                    help="2: each step's encode on one stream and its decode (independent buffers) on a second "
                         "stream, joined once after the timed steps, so short launches overlap each other's "
-                        "ramp-up and drain (default: 2 for the K=3/M=10 workloads cfg2/cfg5, 1 for the bit-sliced "
-                        "wide codes cfg3/cfg4, where co-resident launches measured slower; DESIGN.md section 5)")
+                        "ramp-up and drain (default: 2 for cfg2/cfg4/cfg5, 1 for cfg3, whose bit-sliced launches "
+                        "measured 1-2 %% slower side by side while cfg4's gained 0.6-1.3 %%, "
+                        "profiles/r06_streams_wide_ab.json)")
     p.add_argument("--paired", action="store_true",
                    help="each step as ONE fec_run_batch_jobs call on one stream: its encode and decode share one "
                         "matapply_pair launch where both are register-kernel shapes (cfg2), else one launch each")
@@ -1138,7 +1139,7 @@ def main():
         ns = nstripes
     fresh = args.fresh if args.fresh is not None else (20 if args.workload in ("cfg3", "cfg4") else 0)
     if args.streams is None:
-        args.streams = 1 if args.workload in ("cfg3", "cfg4") or args.paired else 2
+        args.streams = 1 if args.workload == "cfg3" or args.paired else 2
     t = run_workload(k, m, sz, ns, args.steps, args.warmup, dist, use_graph=args.graph, layout=args.layout,
                      streams=args.streams, paired=args.paired,
                      row_padding=not args.no_row_padding, fresh=fresh if rank == 0 else 0)
